@@ -1,0 +1,228 @@
+/*
+ * octpt.h -- C ABI of the MI355X-native octree path-tracing hot path.
+ *
+ * This is the drop-in boundary that replaces the reference's GPU backend
+ * (kekley/octree_pathtracing, src/renderer/gpu_renderer.rs:151-702, implementing
+ * trait RenderingBackend, src/renderer/renderer_trait.rs:19-46).  A Rust host binds
+ * these symbols with an `extern "C"` block and keeps its own
+ * Scene / Octree / Camera types; every struct below is #[repr(C)]-compatible.
+ *
+ * Conventions
+ *  - Every entry returns octpt_status (int32).  No C++ exception crosses the ABI.
+ *  - Input arrays are borrowed for the duration of the call and deep-copied.
+ *  - A context is externally synchronised (one host thread at a time); distinct
+ *    contexts are independent.  Frames returned by octpt_render_async are owned by
+ *    the caller until octpt_frame_release.
+ *  - There is no CPU fallback: without a usable gfx950 device octpt_create fails
+ *    with OCTPT_ERR_DEVICE.
+ */
+#ifndef OCTPT_H
+#define OCTPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCTPT_ABI_VERSION 1u
+
+typedef int32_t octpt_status;
+#define OCTPT_OK 0
+#define OCTPT_ERR_INVALID_ARG 1
+#define OCTPT_ERR_OOM 2
+#define OCTPT_ERR_DEVICE 3
+#define OCTPT_NOT_READY 4     /* FrameInFlightPoll::NotReady (renderer_trait.rs:37-41) */
+#define OCTPT_ERR_UNSUPPORTED 5
+#define OCTPT_CANCELLED 6     /* FrameInFlightPoll::Cancelled */
+#define OCTPT_ERR_INTERNAL 7
+
+typedef struct octpt_ctx octpt_ctx;
+typedef struct octpt_frame octpt_frame;
+typedef struct octpt_octree octpt_octree;
+
+/* new_octree::Octant (src/octree/new_octree.rs:70-74) in C layout, 36 bytes.
+ * child_mask bit i = child i present, bit i+8 = child i is a leaf (the
+ * OctantChildIterator reading, new_octree.rs:84-100).  children[i] is an octant
+ * index (present, not leaf) or the leaf payload (present + leaf).  Child index
+ * i = x | y << 1 | z << 2 (the ESVO/Morton child order, octree_traversal.rs:22-24). */
+typedef struct octpt_octant {
+    uint16_t child_mask;
+    uint16_t reserved;
+    uint32_t children[8];
+} octpt_octant;
+
+/* geometry::sphere::Sphere (src/geometry/sphere.rs:10-14), 32 bytes */
+typedef struct octpt_sphere {
+    float center[3];
+    float radius;
+    uint32_t material;
+    uint32_t reserved[3];
+} octpt_sphere;
+
+/* geometry::cuboid::Cuboid (src/geometry/cuboid.rs:48-52): AABB + one material per face,
+ * Face order West(-X), East(+X), Bottom(-Y), Top(+Y), South(+Z), North(-Z).  48 bytes. */
+typedef struct octpt_cuboid {
+    float min[3];
+    float max[3];
+    uint32_t face_material[6];
+} octpt_cuboid;
+
+/* GPUMaterial (src/gpu_structs/gpu_material.rs:67-76), 32 bytes */
+typedef struct octpt_material {
+    float ior, specular, emittance, roughness, metalness;
+    uint32_t texture_index, tint_index, flags; /* flags: MaterialFlags bits (material.rs:99-108) */
+} octpt_material;
+
+#define OCTPT_TEXTURE_COLOR 0u /* Texture::Color(U8Color)  (texture.rs:15-18) */
+#define OCTPT_TEXTURE_IMAGE 1u /* Texture::Image(RTWImage), RGBA8, row-major, top row first */
+typedef struct octpt_texture {
+    uint32_t kind;
+    uint8_t rgba[4];
+    uint32_t width, height;
+    const uint8_t *pixels; /* width*height*4 bytes for OCTPT_TEXTURE_IMAGE, else NULL */
+} octpt_texture;
+
+/* scene::Sun::new arguments (src/scene/mod.rs:321-330) + SunSamplingStrategy flags (:60-69) */
+typedef struct octpt_sun {
+    float azimuth, altitude, radius;
+    float color[4];
+    float apparent_color[3];
+    int32_t draw_texture, texture_modification;
+    float importance_sample_chance, importance_sample_radius;
+    float luminosity;
+    uint8_t texture_rgba[4];
+    int32_t importance_sampling, diffuse_sun, sun_sampling; /* sun_sampling=1 -> UNSUPPORTED */
+} octpt_sun;
+
+/* Scene (src/scene/mod.rs:146-156) flattened: octree + leaf primitive lists + primitive,
+ * material and texture tables.  Leaf payload p indexes leaf_first/leaf_count; the prims
+ * leaf_prims[first .. first+count) are sphere indices, or cuboid indices | 0x80000000. */
+typedef struct octpt_scene_desc {
+    uint32_t abi_version; /* = OCTPT_ABI_VERSION */
+    const octpt_octant *octants;
+    uint32_t octant_count, root, depth; /* depth <= 21 (new_octree.rs:14); world = [0, 2^depth)^3 */
+    const uint32_t *leaf_first;
+    const uint32_t *leaf_count;
+    uint32_t leaf_table_size;
+    const uint32_t *leaf_prims;
+    uint32_t leaf_prim_count;
+    const octpt_sphere *spheres;
+    uint32_t sphere_count;
+    const octpt_cuboid *cuboids;
+    uint32_t cuboid_count;
+    const octpt_material *materials; /* materials[0] is the outer medium (air) */
+    uint32_t material_count;
+    const octpt_texture *textures;
+    uint32_t texture_count;
+    octpt_sun sun;
+    int32_t emitters_enabled;
+} octpt_scene_desc;
+
+/* renderer::camera::Camera (src/renderer/camera.rs:8-25) */
+typedef struct octpt_camera {
+    float eye[3];
+    float direction[3];
+    float up[3];
+    float fov; /* radians */
+    float aperture, focal_distance; /* must be 0: thin lens is unused by the reference path */
+} octpt_camera;
+
+/* One progressive render call = spp_count passes of TileRenderer::render_tile_average
+ * (tile_renderer.rs:684-734) continuing a running mean that already holds spp_start samples. */
+#define OCTPT_RENDER_SHARD_COMPACT 0x1u /* accum holds only this shard's 8x8 tiles, tile-major */
+typedef struct octpt_render_params {
+    uint32_t width, height;
+    uint32_t spp_start, spp_count;
+    uint32_t max_depth;    /* reference: 5 (path_tracer.rs:56) */
+    uint32_t branch_count; /* only 1 is supported (SURVEY contract C6) */
+    uint32_t seed;
+    uint32_t shard_index, shard_count; /* 8x8 tile t belongs to shard t % shard_count */
+    uint32_t flags;
+} octpt_render_params;
+
+typedef struct octpt_stats {
+    uint64_t paths, segments, esvo_steps, sphere_tests, cuboid_tests, shade_events, texel_reads;
+    uint64_t launches;
+    double kernel_ms; /* HIP-event time of the render kernels since the last reset */
+} octpt_stats;
+
+/* --- library / context ------------------------------------------------------ */
+uint32_t octpt_abi_version(void);
+/* number of visible HIP devices (0 when none) */
+int32_t octpt_device_count(void);
+/* RenderingBackend construction (gpu_renderer.rs:151-200) on HIP device `device` */
+octpt_status octpt_create(int32_t device, octpt_ctx **out);
+void octpt_destroy(octpt_ctx *ctx);
+/* last error message of this context (never NULL) */
+const char *octpt_last_error(const octpt_ctx *ctx);
+
+/* --- RenderingBackend surface ----------------------------------------------- */
+/* set_scene (gpu_renderer.rs:662-669 -> create_pipeline :201-557): validates and uploads */
+octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *scene);
+/* set_camera / get_camera (renderer_trait.rs:20-21) */
+octpt_status octpt_set_camera(octpt_ctx *ctx, const octpt_camera *camera);
+octpt_status octpt_get_camera(const octpt_ctx *ctx, octpt_camera *camera);
+
+/* Synchronous render into host memory.  accum_rgba: width*height*4 floats (or the shard's
+ * compact tiles), in/out running mean, initialise to F32Color::BLACK (0,0,0,1).
+ * out_rgba8 (nullable): tone-mapped U8Color image (colors/mod.rs:408-420) of accum. */
+octpt_status octpt_render(octpt_ctx *ctx, const octpt_render_params *p, float *accum_rgba, uint8_t *out_rgba8);
+
+/* Device-resident render: d_accum is a device pointer (same layout as accum_rgba), the
+ * work is enqueued on `hip_stream` (hipStream_t, NULL = default stream) and not waited for.
+ * d_seg_count (nullable, device, one u32 per accum pixel) receives += ray segments. */
+octpt_status octpt_render_device(octpt_ctx *ctx, const octpt_render_params *p, float *d_accum,
+                                 uint32_t *d_seg_count, void *hip_stream);
+
+/* render_frame (renderer_trait.rs:30-34) -> FrameInFlight (:42-46) */
+octpt_status octpt_render_async(octpt_ctx *ctx, const octpt_render_params *p, float *accum_rgba,
+                                uint8_t *out_rgba8, octpt_frame **out_frame);
+octpt_status octpt_frame_poll(octpt_frame *frame);   /* OK = Ready, NOT_READY, CANCELLED */
+octpt_status octpt_frame_wait(octpt_frame *frame);   /* FrameInFlight::wait_for */
+octpt_status octpt_frame_cancel(octpt_frame *frame); /* result buffers are left untouched */
+void octpt_frame_release(octpt_frame *frame);
+
+/* Tone map a device accumulation buffer into device RGBA8 (colors/mod.rs:408-420). */
+octpt_status octpt_tonemap_device(octpt_ctx *ctx, const float *d_accum, uint8_t *d_rgba8, uint32_t n_pixels,
+                                  void *hip_stream);
+/* Rank 0 of a sharded render: scatter shard_count compact tile buffers (device, concatenated
+ * in shard order, each padded to `shard_stride_pixels`) into a full width*height frame. */
+octpt_status octpt_unshard_device(octpt_ctx *ctx, uint32_t width, uint32_t height, uint32_t shard_count,
+                                  const float *d_shards, uint32_t shard_stride_pixels, float *d_frame,
+                                  void *hip_stream);
+/* pixels a shard owns (its compact buffer length in pixels, tile-padded) */
+uint32_t octpt_shard_pixels(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count);
+
+/* Batch closest-hit query = Scene::hit (scene/mod.rs:172-187) with the octree traversal
+ * (octree_traversal.rs:54-302) restored.  rays: n*6 floats (origin, unit direction), host.
+ * last_prim / last_normal (nullable): self-intersection key per ray.
+ * Outputs (host): t (world, +inf on miss), prim (0xFFFFFFFF on miss), normal n*3 (nullable),
+ * esvo steps (nullable). */
+octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *last_prim, const float *last_normal,
+                             uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps);
+
+octpt_status octpt_get_stats(const octpt_ctx *ctx, octpt_stats *stats);
+octpt_status octpt_reset_stats(octpt_ctx *ctx);
+
+/* --- host octree builder (replaces the Rust-side build for primitive scenes) ---
+ * Voxelises spheres/cuboids into depth-`depth` leaf cells, Morton-sorts
+ * them (new_octree.rs:752-835 code order) and emits octants in pre-order. */
+typedef struct octpt_octree_view {
+    const octpt_octant *octants;
+    uint32_t octant_count, root, depth;
+    const uint32_t *leaf_first, *leaf_count;
+    uint32_t leaf_table_size;
+    const uint32_t *leaf_prims;
+    uint32_t leaf_prim_count;
+} octpt_octree_view;
+octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t sphere_count, const octpt_cuboid *cuboids,
+                                uint32_t cuboid_count, uint32_t depth, octpt_octree **out);
+octpt_status octpt_octree_get_view(const octpt_octree *tree, octpt_octree_view *view);
+void octpt_octree_free(octpt_octree *tree);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCTPT_H */

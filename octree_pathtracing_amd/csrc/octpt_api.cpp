@@ -1,0 +1,907 @@
+// octpt_api.cpp -- host side of the octpt C ABI (include/octpt.h).
+//
+// Replaces the reference's wgpu backend (src/renderer/gpu_renderer.rs:151-702): scene
+// validation + upload (set_scene / create_pipeline), camera uniform construction
+// (render_frame :590-599), progressive render submission, FrameInFlight polling, and the
+// host octree builder for primitive scenes.  No CPU rendering path exists here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/octpt.h"
+#include "octpt_internal.h"
+
+using namespace octpt;
+
+namespace {
+
+constexpr uint32_t kCounterRing = 256;
+
+struct EventPair {
+    hipEvent_t start, stop;
+};
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct octpt_ctx {
+    int device = 0;
+    int num_cu = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // scene
+    bool has_scene = false;
+    DevScene S{};
+    std::vector<void *> scene_allocs;
+    // camera
+    bool has_camera = false;
+    octpt_camera cam{};
+    DevCamera C{};
+    // per-context device state
+    uint32_t *d_counters = nullptr;  // ring of work counters, one per launch
+    uint32_t launch_seq = 0;
+    unsigned long long *d_stats = nullptr;
+    uint8_t *d_lut_byte = nullptr;
+    float *d_lut_float = nullptr;
+    std::vector<EventPair> pending;
+    double kernel_ms = 0.0;
+    uint64_t launches = 0;
+    int blocks_per_cu_cache[kMaxDepth + 1] = {0};
+};
+
+struct octpt_frame {
+    octpt_ctx *ctx = nullptr;
+    hipEvent_t done = nullptr;
+    float *user_accum = nullptr;
+    uint8_t *user_rgba = nullptr;
+    size_t n_pixels = 0;
+    float4 *d_accum = nullptr;
+    uchar4 *d_rgba = nullptr;
+    float *h_accum = nullptr;   // pinned
+    uint8_t *h_rgba = nullptr;  // pinned
+    bool cancelled = false;
+    bool delivered = false;
+};
+
+struct octpt_octree {
+    std::vector<octpt_octant> octants;
+    std::vector<uint32_t> leaf_first, leaf_count, leaf_prims;
+    uint32_t root = 0, depth = 0;
+};
+
+namespace {
+
+octpt_status fail(octpt_ctx *ctx, octpt_status st, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return st;
+}
+
+octpt_status hip_fail(octpt_ctx *ctx, hipError_t e, const char *what) {
+    return fail(ctx, e == hipErrorOutOfMemory ? OCTPT_ERR_OOM : OCTPT_ERR_DEVICE,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(ctx, expr)                                 \
+    do {                                                   \
+        hipError_t _e = (expr);                            \
+        if (_e != hipSuccess) return hip_fail(ctx, _e, #expr); \
+    } while (0)
+
+// colour LUTs (texture.rs:42-62), computed with the host libm like the reference
+void make_luts(float lut_float[256], uint8_t lut_byte[256]) {
+    for (int i = 0; i < 256; ++i) {
+        lut_float[i] = powf((float)i / 255.0f, 2.2f);
+        const float b = powf((float)i / 255.0f, 1.0f / 2.2f) * 255.0f;
+        lut_byte[i] = (uint8_t)(b > 0.0f ? (b >= 255.0f ? 255u : (uint32_t)b) : 0u);
+    }
+}
+
+// glam-order f32 helpers for the host-side uniforms
+inline float dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+inline void cross3(const float a[3], const float b[3], float o[3]) {
+    o[0] = a[1] * b[2] - b[1] * a[2];
+    o[1] = a[2] * b[0] - b[2] * a[0];
+    o[2] = a[0] * b[1] - b[0] * a[1];
+}
+
+// Sun::new (scene/mod.rs:321-383) + diffuse_reflection sun constants (ray/mod.rs:228-259)
+void make_sun(const octpt_sun &p, const float lut_float[256], DevSun &k) {
+    const float theta = p.azimuth, phi = p.altitude;
+    const float r = fabsf(cosf(phi));
+    float sw[3] = {cosf(theta) * r, sinf(phi), sinf(theta) * r};
+    float su[3] = {0.0f, 0.0f, 0.0f};
+    if (fabsf(sw[0]) > 0.1f) su[1] = 1.0f; else su[0] = 1.0f;
+    float sv[3];
+    cross3(sw, su, sv);
+    const float inv = 1.0f / sqrtf(dot3(sv, sv));
+    for (float &c : sv) c = c * inv;
+    cross3(sv, sw, su);
+    std::memcpy(k.sw, sw, sizeof sw);
+    std::memcpy(k.su, su, sizeof su);
+    std::memcpy(k.sv, sv, sizeof sv);
+    k.width = p.radius * 4.0f;
+    k.width2 = k.width * 2.0f;
+    const float gamma_b = powf(1.25f, 2.2f);
+    k.tex[0] = lut_float[p.texture_rgba[0]];
+    k.tex[1] = lut_float[p.texture_rgba[1]];
+    k.tex[2] = lut_float[p.texture_rgba[2]];
+    k.tex[3] = (float)p.texture_rgba[3] / 255.0f;
+    for (int i = 0; i < 3; ++i) {
+        const float atb = (p.texture_modification ? p.apparent_color[i] : 1.0f) * gamma_b;
+        k.isect_mul[i] = atb * 10.0f;
+        k.diffuse_mul[i] = p.color[i] * 10.0f;
+    }
+    k.luminosity = p.luminosity;
+    const float pi = 3.14159265358979323846f;
+    const float az = p.azimuth, alt_fake = p.altitude;
+    const float sgn = std::signbit(alt_fake) ? -1.0f : 1.0f;
+    const float alt = fabsf(alt_fake) > pi / 2.0f ? sgn * pi - alt_fake : alt_fake;
+    k.sun_dx = cosf(az) * cosf(alt);
+    k.sun_dz = sinf(az) * cosf(alt);
+    k.sun_dy = sinf(alt);
+    k.circle_radius = p.radius * p.importance_sample_radius;
+    k.sample_chance = p.importance_sample_chance;
+    k.draw_texture = p.draw_texture ? 1 : 0;
+    k.importance_sampling = p.importance_sampling ? 1 : 0;
+    k.diffuse_sun = p.diffuse_sun ? 1 : 0;
+}
+
+void free_scene(octpt_ctx *ctx) {
+    for (void *p : ctx->scene_allocs) (void)hipFree(p);
+    ctx->scene_allocs.clear();
+    ctx->has_scene = false;
+}
+
+template <class T>
+hipError_t upload(octpt_ctx *ctx, const T *src, size_t n, T **dst) {
+    *dst = nullptr;
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return e;
+    ctx->scene_allocs.push_back(p);
+    if (n && src) {
+        e = hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return e;
+    } else {
+        e = hipMemset(p, 0, bytes);
+        if (e != hipSuccess) return e;
+    }
+    *dst = static_cast<T *>(p);
+    return hipSuccess;
+}
+
+// memoised subtree height with cycle detection; returns -1 on a cycle or bad index
+int subtree_height(const octpt_scene_desc &d, uint32_t node, std::vector<int8_t> &h, int level) {
+    if (level > (int)kMaxDepth + 1) return -1;
+    if (h[node] == -2) return -1;  // on the current DFS path: cycle
+    if (h[node] >= 0) return h[node];
+    h[node] = -2;
+    int best = 1;
+    const octpt_octant &o = d.octants[node];
+    for (int i = 0; i < 8; ++i) {
+        const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+        if (!present || leaf) continue;
+        const int ch = subtree_height(d, o.children[i], h, level + 1);
+        if (ch < 0) return -1;
+        best = std::max(best, ch + 1);
+    }
+    h[node] = (int8_t)best;
+    return best;
+}
+
+octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d) {
+    if (!d) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene is NULL");
+    if (d->abi_version != OCTPT_ABI_VERSION) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene abi_version mismatch");
+    if (d->depth < 1 || d->depth > kMaxDepth) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree depth must be in [1, 21]");
+    if (!d->octants || d->octant_count == 0 || d->root >= d->octant_count)
+        return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree has no root octant");
+    if (d->material_count == 0 || !d->materials) return fail(ctx, OCTPT_ERR_INVALID_ARG, "material table is empty");
+    if (d->texture_count == 0 || !d->textures) return fail(ctx, OCTPT_ERR_INVALID_ARG, "texture table is empty");
+    if (d->leaf_table_size && (!d->leaf_first || !d->leaf_count))
+        return fail(ctx, OCTPT_ERR_INVALID_ARG, "leaf table pointers are NULL");
+    if (d->leaf_prim_count && !d->leaf_prims) return fail(ctx, OCTPT_ERR_INVALID_ARG, "leaf_prims is NULL");
+    if (d->sphere_count && !d->spheres) return fail(ctx, OCTPT_ERR_INVALID_ARG, "spheres is NULL");
+    if (d->cuboid_count && !d->cuboids) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboids is NULL");
+    if (d->sun.sun_sampling)
+        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "sun_sampling (next-event estimation presets FAST/HIGH_QUALITY) is not implemented");
+    for (uint32_t n = 0; n < d->octant_count; ++n) {
+        const octpt_octant &o = d->octants[n];
+        for (int i = 0; i < 8; ++i) {
+            const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+            if (!present) continue;
+            if (leaf && o.children[i] >= d->leaf_table_size)
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "leaf payload " + std::to_string(o.children[i]) + " out of range");
+            if (!leaf && o.children[i] >= d->octant_count)
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "child octant index out of range");
+        }
+    }
+    std::vector<int8_t> h(d->octant_count, -1);
+    const int height = subtree_height(*d, d->root, h, 0);
+    if (height < 0) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree contains a cycle");
+    if ((uint32_t)height > d->depth) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree is deeper than its declared depth");
+    for (uint32_t l = 0; l < d->leaf_table_size; ++l)
+        if ((uint64_t)d->leaf_first[l] + d->leaf_count[l] > d->leaf_prim_count)
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "leaf range exceeds leaf_prims");
+    for (uint32_t k = 0; k < d->leaf_prim_count; ++k) {
+        const uint32_t p = d->leaf_prims[k];
+        if (p & kPrimCuboidBit) {
+            if ((p & ~kPrimCuboidBit) >= d->cuboid_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboid index out of range");
+        } else if (p >= d->sphere_count) {
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "sphere index out of range");
+        }
+    }
+    for (uint32_t s = 0; s < d->sphere_count; ++s)
+        if (d->spheres[s].material >= d->material_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "sphere material out of range");
+    for (uint32_t c = 0; c < d->cuboid_count; ++c)
+        for (int f = 0; f < 6; ++f)
+            if (d->cuboids[c].face_material[f] >= d->material_count)
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboid material out of range");
+    for (uint32_t m = 0; m < d->material_count; ++m)
+        if (d->materials[m].texture_index >= d->texture_count)
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "material texture_index out of range");
+    for (uint32_t t = 0; t < d->texture_count; ++t) {
+        const octpt_texture &x = d->textures[t];
+        if (x.kind == OCTPT_TEXTURE_IMAGE) {
+            if (x.width == 0 || x.height == 0 || !x.pixels)
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "image texture without pixels");
+        } else if (x.kind != OCTPT_TEXTURE_COLOR) {
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "unknown texture kind");
+        }
+    }
+    return OCTPT_OK;
+}
+
+uint32_t tiles_of_shard(uint32_t n_tiles, uint32_t shard, uint32_t count) {
+    return shard < n_tiles ? (n_tiles - shard + count - 1) / count : 0;
+}
+
+octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender &R) {
+    if (!p) return fail(ctx, OCTPT_ERR_INVALID_ARG, "render params NULL");
+    if (!ctx->has_scene) return fail(ctx, OCTPT_ERR_INVALID_ARG, "no scene uploaded (set_scene)");
+    if (!ctx->has_camera) return fail(ctx, OCTPT_ERR_INVALID_ARG, "no camera set");
+    if (p->width == 0 || p->height == 0 || (uint64_t)p->width * p->height >= (1ull << 31))
+        return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad resolution");
+    if (p->max_depth == 0) return fail(ctx, OCTPT_ERR_INVALID_ARG, "max_depth must be >= 1");
+    if (p->branch_count > 1)
+        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "branch_count > 1 is not implemented (SURVEY contract C6)");
+    if (p->shard_count == 0 || p->shard_index >= p->shard_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad shard");
+    if ((uint64_t)p->spp_start + p->spp_count >= (1ull << 24))
+        return fail(ctx, OCTPT_ERR_INVALID_ARG, "spp_start + spp_count must stay below 2^24");
+    R.W = p->width;
+    R.H = p->height;
+    R.spp_start = p->spp_start;
+    R.spp_count = p->spp_count;
+    R.max_depth = p->max_depth;
+    R.seed = p->seed;
+    R.shard_index = p->shard_index;
+    R.shard_count = p->shard_count;
+    R.compact = (p->flags & OCTPT_RENDER_SHARD_COMPACT) ? 1u : 0u;
+    R.tiles_x = (p->width + kTile - 1) / kTile;
+    const uint32_t tiles_y = (p->height + kTile - 1) / kTile;
+    R.shard_tiles = tiles_of_shard(R.tiles_x * tiles_y, p->shard_index, p->shard_count);
+    R.total_items = R.shard_tiles * 64u;
+    R.dim = (float)std::max(p->width, p->height);
+    return OCTPT_OK;
+}
+
+size_t accum_pixels(const DevRender &R) { return R.compact ? (size_t)R.total_items : (size_t)R.W * R.H; }
+
+octpt_status enqueue_render(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s) {
+    if (R.spp_count == 0 || R.total_items == 0) return OCTPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint32_t *counter = ctx->d_counters + (ctx->launch_seq++ % kCounterRing);
+    HIP_TRY(ctx, hipMemsetAsync(counter, 0, sizeof(uint32_t), s));
+    int &bpc = ctx->blocks_per_cu_cache[ctx->S.depth];
+    if (bpc == 0) bpc = render_blocks_per_cu(ctx->S.depth);
+    const uint64_t needed = ((uint64_t)R.total_items + kBlock - 1) / kBlock;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(needed, (uint64_t)ctx->num_cu * bpc));
+    EventPair ev{};
+    HIP_TRY(ctx, hipEventCreate(&ev.start));
+    HIP_TRY(ctx, hipEventCreate(&ev.stop));
+    HIP_TRY(ctx, hipEventRecord(ev.start, s));
+    hipError_t e = launch_render(ctx->S, ctx->C, R, d_accum, d_seg, counter, ctx->d_stats, grid, s);
+    if (e != hipSuccess) {
+        (void)hipEventDestroy(ev.start);
+        (void)hipEventDestroy(ev.stop);
+        return hip_fail(ctx, e, "render_kernel launch");
+    }
+    HIP_TRY(ctx, hipEventRecord(ev.stop, s));
+    ctx->pending.push_back(ev);
+    ctx->launches++;
+    return OCTPT_OK;
+}
+
+void free_frame_buffers(octpt_frame *f) {
+    if (f->d_accum) (void)hipFree(f->d_accum);
+    if (f->d_rgba) (void)hipFree(f->d_rgba);
+    if (f->h_accum) (void)hipHostFree(f->h_accum);
+    if (f->h_rgba) (void)hipHostFree(f->h_rgba);
+    if (f->done) (void)hipEventDestroy(f->done);
+    f->d_accum = nullptr;
+    f->d_rgba = nullptr;
+    f->h_accum = nullptr;
+    f->h_rgba = nullptr;
+    f->done = nullptr;
+}
+
+void deliver(octpt_frame *f) {
+    if (f->delivered || f->cancelled) return;
+    std::memcpy(f->user_accum, f->h_accum, f->n_pixels * 16);
+    if (f->user_rgba) std::memcpy(f->user_rgba, f->h_rgba, f->n_pixels * 4);
+    f->delivered = true;
+}
+
+// ---------------- builder ----------------
+uint64_t part_by_2(uint64_t v) {  // new_octree.rs:813-822
+    uint64_t x = v & 0x1fffff;
+    x = (x | x << 32) & 0x1f00000000ffffULL;
+    x = (x | x << 16) & 0x1f0000ff0000ffULL;
+    x = (x | x << 8) & 0x100f00f00f00f00fULL;
+    x = (x | x << 4) & 0x10c30c30c30c30c3ULL;
+    x = (x | x << 2) & 0x1249249249249249ULL;
+    return x;
+}
+inline uint64_t morton(uint64_t x, uint64_t y, uint64_t z) { return (part_by_2(z) << 2) + (part_by_2(y) << 1) + part_by_2(x); }
+
+struct CellPrim {
+    uint64_t code;
+    uint32_t prim;
+    bool operator<(const CellPrim &o) const { return code != o.code ? code < o.code : prim < o.prim; }
+};
+
+struct Builder {
+    octpt_octree *t;
+    std::vector<uint64_t> leaf_code;
+    uint32_t depth;
+    uint32_t node(uint32_t level, uint32_t lo, uint32_t hi) {
+        const uint32_t id = (uint32_t)t->octants.size();
+        t->octants.push_back(octpt_octant{0, 0, {0, 0, 0, 0, 0, 0, 0, 0}});
+        const uint32_t shift = 3 * (depth - 1 - level);
+        uint32_t a = lo;
+        for (uint32_t c = 0; c < 8; ++c) {
+            uint32_t b = a;
+            while (b < hi && ((leaf_code[b] >> shift) & 7u) == c) ++b;
+            if (b == a) continue;
+            if (level + 1 == depth) {
+                t->octants[id].child_mask |= (uint16_t)((1u << c) | (1u << (c + 8)));
+                t->octants[id].children[c] = a;
+            } else {
+                const uint32_t ch = node(level + 1, a, b);
+                t->octants[id].child_mask |= (uint16_t)(1u << c);
+                t->octants[id].children[c] = ch;
+            }
+            a = b;
+        }
+        return id;
+    }
+};
+
+inline int32_t clamp_cell(float f, int32_t hi) {
+    if (!(f >= 0.0f)) return 0;  // also NaN
+    if (f >= (float)hi) return hi;
+    return (int32_t)f;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t octpt_abi_version(void) { return OCTPT_ABI_VERSION; }
+
+int32_t octpt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+octpt_status octpt_create(int32_t device, octpt_ctx **out) {
+    if (!out) return OCTPT_ERR_INVALID_ARG;
+    *out = nullptr;
+    octpt_ctx *ctx = new (std::nothrow) octpt_ctx();
+    if (!ctx) return OCTPT_ERR_OOM;
+    auto bail = [&](octpt_status st) {
+        octpt_destroy(ctx);
+        return st;
+    };
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return bail(OCTPT_ERR_DEVICE);
+    if (device < 0 || device >= n) return bail(OCTPT_ERR_INVALID_ARG);
+    hipDeviceProp_t prop{};
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return bail(OCTPT_ERR_DEVICE);
+    ctx->device = device;
+    ctx->num_cu = prop.multiProcessorCount;
+    if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);
+    if (hipMalloc(&ctx->d_stats, kStatCount * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_OOM);
+    if (hipMemset(ctx->d_stats, 0, kStatCount * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    float lf[256];
+    uint8_t lb[256];
+    make_luts(lf, lb);
+    if (hipMalloc(&ctx->d_lut_float, sizeof lf) != hipSuccess) return bail(OCTPT_ERR_OOM);
+    if (hipMalloc(&ctx->d_lut_byte, sizeof lb) != hipSuccess) return bail(OCTPT_ERR_OOM);
+    if (hipMemcpy(ctx->d_lut_float, lf, sizeof lf, hipMemcpyHostToDevice) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    if (hipMemcpy(ctx->d_lut_byte, lb, sizeof lb, hipMemcpyHostToDevice) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    *out = ctx;
+    return OCTPT_OK;
+}
+
+void octpt_destroy(octpt_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &e : ctx->pending) {
+        (void)hipEventSynchronize(e.stop);
+        (void)hipEventDestroy(e.start);
+        (void)hipEventDestroy(e.stop);
+    }
+    free_scene(ctx);
+    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_stats) (void)hipFree(ctx->d_stats);
+    if (ctx->d_lut_float) (void)hipFree(ctx->d_lut_float);
+    if (ctx->d_lut_byte) (void)hipFree(ctx->d_lut_byte);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *octpt_last_error(const octpt_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    try {
+        octpt_status st = validate_scene(ctx, d);
+        if (st != OCTPT_OK) return st;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        free_scene(ctx);
+        DevScene S{};
+        std::vector<uint32_t> mask(d->octant_count), children((size_t)d->octant_count * 8);
+        for (uint32_t n = 0; n < d->octant_count; ++n) {
+            mask[n] = d->octants[n].child_mask;
+            std::memcpy(&children[(size_t)n * 8], d->octants[n].children, 32);
+        }
+        std::vector<uint2> ranges(d->leaf_table_size);
+        for (uint32_t l = 0; l < d->leaf_table_size; ++l) ranges[l] = make_uint2(d->leaf_first[l], d->leaf_count[l]);
+        std::vector<float4> sph(d->sphere_count);
+        std::vector<uint32_t> sph_mat(d->sphere_count);
+        for (uint32_t s = 0; s < d->sphere_count; ++s) {
+            const octpt_sphere &x = d->spheres[s];
+            sph[s] = make_float4(x.center[0], x.center[1], x.center[2], x.radius);
+            sph_mat[s] = x.material;
+        }
+        std::vector<float4> cmin(d->cuboid_count), cmax(d->cuboid_count);
+        std::vector<uint32_t> cmat((size_t)d->cuboid_count * 6);
+        for (uint32_t c = 0; c < d->cuboid_count; ++c) {
+            const octpt_cuboid &x = d->cuboids[c];
+            cmin[c] = make_float4(x.min[0], x.min[1], x.min[2], 0.0f);
+            cmax[c] = make_float4(x.max[0], x.max[1], x.max[2], 0.0f);
+            std::memcpy(&cmat[(size_t)c * 6], x.face_material, 24);
+        }
+        std::vector<DevMaterial> mats(d->material_count);
+        for (uint32_t m = 0; m < d->material_count; ++m) {
+            const octpt_material &x = d->materials[m];
+            mats[m] = DevMaterial{x.ior, x.specular, x.emittance, x.roughness, x.metalness, x.texture_index, x.tint_index, x.flags};
+        }
+        std::vector<DevTexture> texs(d->texture_count);
+        std::vector<uint8_t> texels;
+        for (uint32_t t = 0; t < d->texture_count; ++t) {
+            const octpt_texture &x = d->textures[t];
+            DevTexture dt{};
+            dt.kind = x.kind;
+            dt.rgba = (uint32_t)x.rgba[0] | ((uint32_t)x.rgba[1] << 8) | ((uint32_t)x.rgba[2] << 16) | ((uint32_t)x.rgba[3] << 24);
+            if (x.kind == OCTPT_TEXTURE_IMAGE) {
+                dt.width = x.width;
+                dt.height = x.height;
+                dt.offset = texels.size();
+                texels.insert(texels.end(), x.pixels, x.pixels + (size_t)x.width * x.height * 4);
+            }
+            texs[t] = dt;
+        }
+        uint32_t *d_mask, *d_children, *d_prims, *d_sph_mat, *d_cmat;
+        uint2 *d_ranges;
+        float4 *d_sph, *d_cmin, *d_cmax;
+        DevMaterial *d_mats;
+        DevTexture *d_texs;
+        uint8_t *d_texels;
+        HIP_TRY(ctx, upload(ctx, mask.data(), mask.size(), &d_mask));
+        HIP_TRY(ctx, upload(ctx, children.data(), children.size(), &d_children));
+        HIP_TRY(ctx, upload(ctx, ranges.data(), ranges.size(), &d_ranges));
+        HIP_TRY(ctx, upload(ctx, d->leaf_prims, d->leaf_prim_count, &d_prims));
+        HIP_TRY(ctx, upload(ctx, sph.data(), sph.size(), &d_sph));
+        HIP_TRY(ctx, upload(ctx, sph_mat.data(), sph_mat.size(), &d_sph_mat));
+        HIP_TRY(ctx, upload(ctx, cmin.data(), cmin.size(), &d_cmin));
+        HIP_TRY(ctx, upload(ctx, cmax.data(), cmax.size(), &d_cmax));
+        HIP_TRY(ctx, upload(ctx, cmat.data(), cmat.size(), &d_cmat));
+        HIP_TRY(ctx, upload(ctx, mats.data(), mats.size(), &d_mats));
+        HIP_TRY(ctx, upload(ctx, texs.data(), texs.size(), &d_texs));
+        HIP_TRY(ctx, upload(ctx, texels.data(), texels.size(), &d_texels));
+        S.node_mask = d_mask;
+        S.node_children = d_children;
+        S.root = d->root;
+        S.depth = d->depth;
+        S.n_octants = d->octant_count;
+        S.octree_scale = ldexpf(1.0f, -(int)d->depth);  // Octree::scale (new_octree.rs:40-42)
+        S.leaf_range = d_ranges;
+        S.leaf_prims = d_prims;
+        S.spheres = d_sph;
+        S.sphere_mat = d_sph_mat;
+        S.cub_min = d_cmin;
+        S.cub_max = d_cmax;
+        S.cub_mat = d_cmat;
+        S.mats = d_mats;
+        S.texs = d_texs;
+        S.texels = d_texels;
+        S.lut_float = ctx->d_lut_float;
+        float lf[256];
+        uint8_t lb[256];
+        make_luts(lf, lb);
+        make_sun(d->sun, lf, S.sun);
+        S.emitters = d->emitters_enabled ? 1 : 0;
+        ctx->S = S;
+        ctx->has_scene = true;
+        return OCTPT_OK;
+    } catch (const std::bad_alloc &) {
+        free_scene(ctx);
+        return fail(ctx, OCTPT_ERR_OOM, "host allocation failed");
+    } catch (...) {
+        free_scene(ctx);
+        return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in scene upload");
+    }
+}
+
+octpt_status octpt_set_camera(octpt_ctx *ctx, const octpt_camera *c) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    if (!c) return fail(ctx, OCTPT_ERR_INVALID_ARG, "camera NULL");
+    if (!(c->fov > 0.0f && c->fov < 3.14159265f)) return fail(ctx, OCTPT_ERR_INVALID_ARG, "fov must be in (0, pi)");
+    if (c->aperture != 0.0f) return fail(ctx, OCTPT_ERR_UNSUPPORTED, "thin-lens aperture is not used by the reference path");
+    ctx->cam = *c;
+    DevCamera C{};
+    std::memcpy(C.eye, c->eye, 12);
+    std::memcpy(C.dir, c->direction, 12);
+    std::memcpy(C.up, c->up, 12);
+    cross3(c->direction, c->up, C.right);            // camera.rs:80
+    C.d_factor = 1.0f / tanf(c->fov / 2.0f);         // camera.rs:79
+    ctx->C = C;
+    ctx->has_camera = true;
+    return OCTPT_OK;
+}
+
+octpt_status octpt_get_camera(const octpt_ctx *ctx, octpt_camera *c) {
+    if (!ctx || !c) return OCTPT_ERR_INVALID_ARG;
+    if (!ctx->has_camera) return OCTPT_ERR_INVALID_ARG;
+    *c = ctx->cam;
+    return OCTPT_OK;
+}
+
+octpt_status octpt_render_device(octpt_ctx *ctx, const octpt_render_params *p, float *d_accum, uint32_t *d_seg,
+                                 void *stream) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    if (!d_accum) return fail(ctx, OCTPT_ERR_INVALID_ARG, "d_accum NULL");
+    try {
+        DevRender R{};
+        octpt_status st = make_render(ctx, p, R);
+        if (st != OCTPT_OK) return st;
+        return enqueue_render(ctx, R, reinterpret_cast<float4 *>(d_accum), d_seg, static_cast<hipStream_t>(stream));
+    } catch (...) {
+        return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in render");
+    }
+}
+
+octpt_status octpt_render_async(octpt_ctx *ctx, const octpt_render_params *p, float *accum, uint8_t *rgba,
+                                octpt_frame **out) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    if (!out || !accum) return fail(ctx, OCTPT_ERR_INVALID_ARG, "NULL output");
+    *out = nullptr;
+    octpt_frame *f = nullptr;
+    try {
+        DevRender R{};
+        octpt_status st = make_render(ctx, p, R);
+        if (st != OCTPT_OK) return st;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        f = new octpt_frame();
+        f->ctx = ctx;
+        f->user_accum = accum;
+        f->user_rgba = rgba;
+        f->n_pixels = accum_pixels(R);
+        auto fail_frame = [&](hipError_t e, const char *what) {
+            free_frame_buffers(f);
+            delete f;
+            return hip_fail(ctx, e, what);
+        };
+        hipError_t e;
+        if ((e = hipMalloc(&f->d_accum, f->n_pixels * 16)) != hipSuccess) return fail_frame(e, "hipMalloc accum");
+        if ((e = hipHostMalloc(&f->h_accum, f->n_pixels * 16, hipHostMallocDefault)) != hipSuccess)
+            return fail_frame(e, "hipHostMalloc accum");
+        if (rgba) {
+            if ((e = hipMalloc(&f->d_rgba, f->n_pixels * 4)) != hipSuccess) return fail_frame(e, "hipMalloc rgba");
+            if ((e = hipHostMalloc(&f->h_rgba, f->n_pixels * 4, hipHostMallocDefault)) != hipSuccess)
+                return fail_frame(e, "hipHostMalloc rgba");
+        }
+        if ((e = hipEventCreateWithFlags(&f->done, hipEventDisableTiming)) != hipSuccess) return fail_frame(e, "event");
+        std::memcpy(f->h_accum, accum, f->n_pixels * 16);
+        if ((e = hipMemcpyAsync(f->d_accum, f->h_accum, f->n_pixels * 16, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+            return fail_frame(e, "H2D accum");
+        st = enqueue_render(ctx, R, f->d_accum, nullptr, ctx->stream);
+        if (st != OCTPT_OK) {
+            (void)hipStreamSynchronize(ctx->stream);
+            free_frame_buffers(f);
+            delete f;
+            return st;
+        }
+        if (rgba) {
+            if ((e = launch_tonemap(f->d_accum, f->d_rgba, (uint32_t)f->n_pixels, ctx->d_lut_byte, ctx->stream)) != hipSuccess)
+                return fail_frame(e, "tonemap launch");
+            if ((e = hipMemcpyAsync(f->h_rgba, f->d_rgba, f->n_pixels * 4, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+                return fail_frame(e, "D2H rgba");
+        }
+        if ((e = hipMemcpyAsync(f->h_accum, f->d_accum, f->n_pixels * 16, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+            return fail_frame(e, "D2H accum");
+        if ((e = hipEventRecord(f->done, ctx->stream)) != hipSuccess) return fail_frame(e, "event record");
+        *out = f;
+        return OCTPT_OK;
+    } catch (...) {
+        if (f) {
+            free_frame_buffers(f);
+            delete f;
+        }
+        return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in render_async");
+    }
+}
+
+octpt_status octpt_frame_poll(octpt_frame *f) {
+    if (!f) return OCTPT_ERR_INVALID_ARG;
+    if (f->cancelled) return OCTPT_CANCELLED;
+    if (f->delivered) return OCTPT_OK;
+    const hipError_t e = hipEventQuery(f->done);
+    if (e == hipErrorNotReady) return OCTPT_NOT_READY;
+    if (e != hipSuccess) return hip_fail(f->ctx, e, "frame poll");
+    deliver(f);
+    return OCTPT_OK;
+}
+
+octpt_status octpt_frame_wait(octpt_frame *f) {
+    if (!f) return OCTPT_ERR_INVALID_ARG;
+    if (f->cancelled) return OCTPT_CANCELLED;
+    if (!f->delivered) {
+        const hipError_t e = hipEventSynchronize(f->done);
+        if (e != hipSuccess) return hip_fail(f->ctx, e, "frame wait");
+        deliver(f);
+    }
+    return OCTPT_OK;
+}
+
+octpt_status octpt_frame_cancel(octpt_frame *f) {
+    if (!f) return OCTPT_ERR_INVALID_ARG;
+    if (!f->delivered) f->cancelled = true;
+    return OCTPT_OK;
+}
+
+void octpt_frame_release(octpt_frame *f) {
+    if (!f) return;
+    if (f->done) (void)hipEventSynchronize(f->done);  // buffers may still be in use by the stream
+    free_frame_buffers(f);
+    delete f;
+}
+
+octpt_status octpt_render(octpt_ctx *ctx, const octpt_render_params *p, float *accum, uint8_t *rgba) {
+    octpt_frame *f = nullptr;
+    octpt_status st = octpt_render_async(ctx, p, accum, rgba, &f);
+    if (st != OCTPT_OK) return st;
+    st = octpt_frame_wait(f);
+    octpt_frame_release(f);
+    return st;
+}
+
+octpt_status octpt_tonemap_device(octpt_ctx *ctx, const float *d_accum, uint8_t *d_rgba, uint32_t n, void *stream) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    if (!d_accum || !d_rgba) return fail(ctx, OCTPT_ERR_INVALID_ARG, "NULL buffer");
+    if (n == 0) return OCTPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, launch_tonemap(reinterpret_cast<const float4 *>(d_accum), reinterpret_cast<uchar4 *>(d_rgba), n,
+                                ctx->d_lut_byte, static_cast<hipStream_t>(stream)));
+    return OCTPT_OK;
+}
+
+uint32_t octpt_shard_pixels(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count) {
+    if (shard_count == 0 || shard_index >= shard_count) return 0;
+    const uint32_t tiles = ((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
+    return tiles_of_shard(tiles, shard_index, shard_count) * 64u;
+}
+
+octpt_status octpt_unshard_device(octpt_ctx *ctx, uint32_t W, uint32_t H, uint32_t N, const float *d_shards,
+                                  uint32_t stride, float *d_frame, void *stream) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    if (!d_shards || !d_frame || N == 0 || W == 0 || H == 0) return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad unshard args");
+    if (stride < octpt_shard_pixels(W, H, 0, N)) return fail(ctx, OCTPT_ERR_INVALID_ARG, "shard stride too small");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, launch_unshard(W, H, N, reinterpret_cast<const float4 *>(d_shards), stride,
+                                reinterpret_cast<float4 *>(d_frame), static_cast<hipStream_t>(stream)));
+    return OCTPT_OK;
+}
+
+octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *last_prim, const float *last_normal,
+                             uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    if (!ctx->has_scene) return fail(ctx, OCTPT_ERR_INVALID_ARG, "no scene uploaded");
+    if (n == 0) return OCTPT_OK;
+    if (!rays || !t || !prim) return fail(ctx, OCTPT_ERR_INVALID_ARG, "NULL buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    float *d_rays = nullptr, *d_ln = nullptr, *d_t = nullptr, *d_n = nullptr;
+    uint32_t *d_lp = nullptr, *d_p = nullptr, *d_s = nullptr;
+    auto cleanup = [&]() {
+        for (void *q : {(void *)d_rays, (void *)d_ln, (void *)d_t, (void *)d_n, (void *)d_lp, (void *)d_p, (void *)d_s})
+            if (q) (void)hipFree(q);
+    };
+    hipError_t e = hipSuccess;
+    do {
+        if ((e = hipMalloc(&d_rays, (size_t)n * 24)) != hipSuccess) break;
+        if ((e = hipMemcpy(d_rays, rays, (size_t)n * 24, hipMemcpyHostToDevice)) != hipSuccess) break;
+        if (last_prim) {
+            if ((e = hipMalloc(&d_lp, (size_t)n * 4)) != hipSuccess) break;
+            if ((e = hipMemcpy(d_lp, last_prim, (size_t)n * 4, hipMemcpyHostToDevice)) != hipSuccess) break;
+        }
+        if (last_normal) {
+            if ((e = hipMalloc(&d_ln, (size_t)n * 12)) != hipSuccess) break;
+            if ((e = hipMemcpy(d_ln, last_normal, (size_t)n * 12, hipMemcpyHostToDevice)) != hipSuccess) break;
+        }
+        if ((e = hipMalloc(&d_t, (size_t)n * 4)) != hipSuccess) break;
+        if ((e = hipMalloc(&d_p, (size_t)n * 4)) != hipSuccess) break;
+        if (normal && (e = hipMalloc(&d_n, (size_t)n * 12)) != hipSuccess) break;
+        if (steps && (e = hipMalloc(&d_s, (size_t)n * 4)) != hipSuccess) break;
+        if ((e = launch_intersect(ctx->S, d_rays, d_lp, d_ln, n, d_t, d_p, d_n, d_s, ctx->stream)) != hipSuccess) break;
+        if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) break;
+        if ((e = hipMemcpy(t, d_t, (size_t)n * 4, hipMemcpyDeviceToHost)) != hipSuccess) break;
+        if ((e = hipMemcpy(prim, d_p, (size_t)n * 4, hipMemcpyDeviceToHost)) != hipSuccess) break;
+        if (normal && (e = hipMemcpy(normal, d_n, (size_t)n * 12, hipMemcpyDeviceToHost)) != hipSuccess) break;
+        if (steps && (e = hipMemcpy(steps, d_s, (size_t)n * 4, hipMemcpyDeviceToHost)) != hipSuccess) break;
+    } while (0);
+    cleanup();
+    if (e != hipSuccess) return hip_fail(ctx, e, "intersect");
+    return OCTPT_OK;
+}
+
+octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
+    if (!cctx || !out) return OCTPT_ERR_INVALID_ARG;
+    octpt_ctx *ctx = const_cast<octpt_ctx *>(cctx);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (auto &e : ctx->pending) {
+        HIP_TRY(ctx, hipEventSynchronize(e.stop));
+        float ms = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, e.start, e.stop));
+        ctx->kernel_ms += ms;
+        (void)hipEventDestroy(e.start);
+        (void)hipEventDestroy(e.stop);
+    }
+    ctx->pending.clear();
+    unsigned long long v[kStatCount];
+    HIP_TRY(ctx, hipMemcpy(v, ctx->d_stats, sizeof v, hipMemcpyDeviceToHost));
+    out->paths = v[kStatPaths];
+    out->segments = v[kStatSegments];
+    out->esvo_steps = v[kStatSteps];
+    out->sphere_tests = v[kStatSphereTests];
+    out->cuboid_tests = v[kStatCuboidTests];
+    out->shade_events = v[kStatShade];
+    out->texel_reads = v[kStatTexels];
+    out->launches = ctx->launches;
+    out->kernel_ms = ctx->kernel_ms;
+    return OCTPT_OK;
+}
+
+octpt_status octpt_reset_stats(octpt_ctx *ctx) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    octpt_stats tmp;
+    octpt_status st = octpt_get_stats(ctx, &tmp);  // drains pending events
+    if (st != OCTPT_OK) return st;
+    HIP_TRY(ctx, hipMemset(ctx->d_stats, 0, kStatCount * sizeof(unsigned long long)));
+    ctx->kernel_ms = 0.0;
+    ctx->launches = 0;
+    return OCTPT_OK;
+}
+
+octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const octpt_cuboid *cuboids, uint32_t nc,
+                                uint32_t depth, octpt_octree **out) {
+    if (!out) return OCTPT_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (depth < 1 || depth > kMaxDepth) return OCTPT_ERR_INVALID_ARG;
+    if ((ns && !spheres) || (nc && !cuboids)) return OCTPT_ERR_INVALID_ARG;
+    try {
+        const int32_t N = 1 << depth;
+        std::vector<CellPrim> cells;
+        for (uint32_t i = 0; i < ns; ++i) {
+            const float *c = spheres[i].center;
+            const float r = spheres[i].radius;
+            if (!(r > 0.0f)) continue;
+            int32_t lo[3], hi[3];
+            bool empty = false;
+            for (int a = 0; a < 3; ++a) {
+                const float fl = floorf(c[a] - r), fh = floorf(c[a] + r);
+                if (fh < 0.0f || fl > (float)(N - 1)) empty = true;
+                lo[a] = clamp_cell(fl, N - 1);
+                hi[a] = clamp_cell(fh, N - 1);
+            }
+            if (empty) continue;
+            const float r2 = r * r;
+            for (int32_t z = lo[2]; z <= hi[2]; ++z)
+                for (int32_t y = lo[1]; y <= hi[1]; ++y)
+                    for (int32_t x = lo[0]; x <= hi[0]; ++x) {
+                        const float bl[3] = {(float)x, (float)y, (float)z};
+                        float dd[3];
+                        for (int a = 0; a < 3; ++a) {
+                            const float l = bl[a], h = bl[a] + 1.0f;
+                            dd[a] = c[a] < l ? l - c[a] : (c[a] > h ? c[a] - h : 0.0f);
+                        }
+                        if ((dd[0] * dd[0] + dd[1] * dd[1]) + dd[2] * dd[2] <= r2)
+                            cells.push_back(CellPrim{morton((uint64_t)x, (uint64_t)y, (uint64_t)z), i});
+                    }
+        }
+        for (uint32_t i = 0; i < nc; ++i) {
+            const octpt_cuboid &b = cuboids[i];
+            int32_t lo[3], hi[3];
+            bool empty = false;
+            for (int a = 0; a < 3; ++a) {
+                const float fl = floorf(b.min[a]), fh = floorf(b.max[a]);
+                if (fh < 0.0f || fl > (float)(N - 1) || b.max[a] < b.min[a]) empty = true;
+                lo[a] = clamp_cell(fl, N - 1);
+                hi[a] = clamp_cell(fh, N - 1);
+            }
+            if (empty) continue;
+            for (int32_t z = lo[2]; z <= hi[2]; ++z)
+                for (int32_t y = lo[1]; y <= hi[1]; ++y)
+                    for (int32_t x = lo[0]; x <= hi[0]; ++x)
+                        cells.push_back(CellPrim{morton((uint64_t)x, (uint64_t)y, (uint64_t)z), i | kPrimCuboidBit});
+        }
+        std::sort(cells.begin(), cells.end());
+        octpt_octree *t = new octpt_octree();
+        t->depth = depth;
+        std::vector<uint64_t> codes;
+        t->leaf_prims.resize(cells.size());
+        for (size_t k = 0; k < cells.size(); ++k) {
+            if (k == 0 || cells[k].code != cells[k - 1].code) {
+                t->leaf_first.push_back((uint32_t)k);
+                t->leaf_count.push_back(0);
+                codes.push_back(cells[k].code);
+            }
+            t->leaf_count.back()++;
+            t->leaf_prims[k] = cells[k].prim;
+        }
+        Builder b{t, std::move(codes), depth};
+        t->root = b.node(0, 0, (uint32_t)b.leaf_code.size());
+        *out = t;
+        return OCTPT_OK;
+    } catch (const std::bad_alloc &) {
+        return OCTPT_ERR_OOM;
+    } catch (...) {
+        return OCTPT_ERR_INTERNAL;
+    }
+}
+
+octpt_status octpt_octree_get_view(const octpt_octree *t, octpt_octree_view *v) {
+    if (!t || !v) return OCTPT_ERR_INVALID_ARG;
+    v->octants = t->octants.data();
+    v->octant_count = (uint32_t)t->octants.size();
+    v->root = t->root;
+    v->depth = t->depth;
+    v->leaf_first = t->leaf_first.data();
+    v->leaf_count = t->leaf_count.data();
+    v->leaf_table_size = (uint32_t)t->leaf_first.size();
+    v->leaf_prims = t->leaf_prims.data();
+    v->leaf_prim_count = (uint32_t)t->leaf_prims.size();
+    return OCTPT_OK;
+}
+
+void octpt_octree_free(octpt_octree *t) { delete t; }
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+// octpt_internal.h -- device-side scene layout shared by the host API (octpt_api.cpp) and
+// the gfx950 kernels (octpt_kernels.hip).  Layout notes live in DESIGN.md §5.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace octpt {
+
+constexpr uint32_t kPrimNone = 0xFFFFFFFFu;
+constexpr uint32_t kPrimCuboidBit = 0x80000000u;
+constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primary rays
+constexpr uint32_t kBlock = 256;       // threads per block (4 waves)
+constexpr uint32_t kMaxDepth = 21;     // new_octree.rs:14
+
+// GPUMaterial (gpu_material.rs:67-76), 32 B: fetched as two float4
+struct alignas(16) DevMaterial {
+    float ior, specular, emittance, roughness;
+    float metalness;
+    uint32_t texture_index, tint_index, flags;
+};
+
+// texture table entry, 16 B
+struct alignas(16) DevTexture {
+    uint32_t kind;      // 0 colour, 1 image
+    uint32_t rgba;      // packed U8Color (r | g<<8 | b<<16 | a<<24) for kind 0
+    uint32_t width;     // image only
+    uint32_t height;
+    uint64_t offset;    // byte offset in the texel pool
+    uint64_t pad;
+};
+
+// Sun::new derived constants (scene/mod.rs:321-383) + diffuse_reflection importance
+// sampling constants (ray/mod.rs:228-259); computed once on the host with libm.
+struct DevSun {
+    float sw[3], su[3], sv[3];
+    float width, width2;
+    float tex[4];
+    float isect_mul[3];
+    float diffuse_mul[3];
+    float luminosity;
+    float sun_dx, sun_dy, sun_dz;
+    float circle_radius, sample_chance;
+    int32_t draw_texture, importance_sampling, diffuse_sun;
+};
+
+struct DevScene {
+    const uint32_t *node_mask;      // per octant: child_mask (bit i present, bit i+8 leaf)
+    const uint32_t *node_children;  // 8 per octant
+    uint32_t root, depth, n_octants;
+    float octree_scale;             // 2^-depth
+    const uint2 *leaf_range;        // (first, count) per leaf payload
+    const uint32_t *leaf_prims;
+    const float4 *spheres;          // (cx, cy, cz, r)
+    const uint32_t *sphere_mat;
+    const float4 *cub_min;          // (x, y, z, -)
+    const float4 *cub_max;
+    const uint32_t *cub_mat;        // 6 per cuboid
+    const DevMaterial *mats;
+    const DevTexture *texs;
+    const uint8_t *texels;
+    const float *lut_float;         // LUT_TABLE_FLOAT (texture.rs:51-54)
+    DevSun sun;
+    int32_t emitters;
+};
+
+struct DevCamera {
+    float eye[3], dir[3], right[3], up[3];
+    float d_factor;  // 1 / tan(fov / 2)  (camera.rs:79)
+};
+
+struct DevRender {
+    uint32_t W, H;
+    uint32_t spp_start, spp_count;
+    uint32_t max_depth;
+    uint32_t seed;
+    uint32_t shard_index, shard_count;
+    uint32_t compact;        // accum holds the shard's tiles only (tile-major)
+    uint32_t tiles_x;        // ceil(W / 8)
+    uint32_t shard_tiles;    // tiles owned by this shard
+    uint32_t total_items;    // shard_tiles * 64 work items
+    float dim;               // max(W, H)
+};
+
+// per-launch statistics, accumulated with one atomic per wave
+enum StatIndex {
+    kStatPaths = 0,
+    kStatSegments,
+    kStatSteps,
+    kStatSphereTests,
+    kStatCuboidTests,
+    kStatShade,
+    kStatTexels,
+    kStatCount
+};
+
+// kernel launchers (octpt_kernels.hip)
+hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
+                         uint32_t *segcount, uint32_t *counter, unsigned long long *stats, int grid,
+                         hipStream_t stream);
+hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t *last_prim,
+                            const float *last_normal, uint32_t n, float *t, uint32_t *prim, float *normal,
+                            uint32_t *steps, hipStream_t stream);
+hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const uint8_t *lut_byte,
+                          hipStream_t stream);
+hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards,
+                          uint32_t stride, float4 *frame, hipStream_t stream);
+int render_blocks_per_cu(uint32_t depth);
+size_t render_lds_bytes(uint32_t depth);
+
+}  // namespace octpt

@@ -1,0 +1,964 @@
+// octpt_kernels.hip -- gfx950 (CDNA4) kernels of the octree path-tracing hot path.
+//
+// render_kernel is a persistent wavefront megakernel.  Every lane owns one pixel at a
+// time and runs that pixel's progressive passes (TileRenderer::render_tile_average,
+// reference src/renderer/tile_renderer.rs:684-734) back to back; a lane is in one of a
+// few states (new path / segment setup / ESVO traversal / shading / refill) and the wave
+// keeps traversing while at least half of its live lanes are traversing, then shades the
+// lanes that finished their segment (wave-level ballot compaction).  Lanes
+// that finish a pixel pull the next work item from a device atomic counter (64 work items
+// = one 8x8 screen tile per wave).  The ESVO stack lives in LDS (one 8-byte slot per
+// octree level per lane, [slot][lane] so a wave's access is one conflict-free row).
+//
+// Float semantics follow the oracle (oracle/cpu_ref.c) bit for bit: -ffp-contract=off,
+// correctly rounded div/sqrt, the portable f32 math below, and the
+// reference's operation order.  The only difference is the radiance accumulation order
+// (forward throughput instead of the reference's recursion), which the oracle also
+// implements as `forward_accumulation`.
+#include "octpt_internal.h"
+
+namespace octpt {
+namespace {
+
+#define RAY_EPSILON 0.00000005f
+#define RAY_OFFSET 0.000001f
+#define OCTREE_MAX_STEPS 1000u
+#define OCTREE_MAX_SCALE 23u
+#define OCTREE_EPSILON 1.1920929e-7f
+#define MAX_DST_WORLD 1024.0f
+#define PI_F 3.14159265358979323846f
+#define CELL_TOL 0.001f
+#define SUN_MAX_CHANCE 0.9f
+#define MAT_FLAG_REFRACTIVE 0x4u
+#define MAX_PATH_SEGMENTS 64u  // [C15] next_intersection calls per path (grazing self-hit loops)
+
+// ---------------------------------------------------------------------------
+// f32 vector helpers (glam Vec3A operation order, see oracle/cpu_ref.c)
+// ---------------------------------------------------------------------------
+struct v3 {
+    float x, y, z;
+};
+__device__ __forceinline__ v3 V(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ v3 vscale(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float vdot(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ v3 vcross(v3 a, v3 b) {
+    return V(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+__device__ __forceinline__ v3 vnorm(v3 a) {
+    float r = 1.0f / sqrtf(vdot(a, a));
+    return vscale(a, r);
+}
+__device__ __forceinline__ float fmn(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float fmx(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float vmin3(v3 a) { return fmn(fmn(a.x, a.y), a.z); }
+__device__ __forceinline__ float vmax3(v3 a) { return fmx(fmx(a.x, a.y), a.z); }
+__device__ __forceinline__ float signum_(float f) { return (__float_as_uint(f) >> 31) ? -1.0f : 1.0f; }
+
+// ---------------------------------------------------------------------------
+// portable f32 math -- identical constants and order to the oracle
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void dm_sincos(float x, float &s, float &c) {
+    const float kf = floorf(x * 0.636619772367581343f + 0.5f);
+    const int k = (int)kf;
+    const float r = ((x - kf * 1.5703125f) - kf * 4.837512969970703125e-4f) - kf * 7.54978995489188216e-8f;
+    const float z = r * r;
+    const float sp = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
+    const float cp = (1.0f - 0.5f * z) +
+                     z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f));
+    switch (k & 3) {
+    case 0: s = sp; c = cp; break;
+    case 1: s = cp; c = -sp; break;
+    case 2: s = -sp; c = -cp; break;
+    default: s = -cp; c = sp; break;
+    }
+}
+__device__ __forceinline__ float dm_cos(float x) { float s, c; dm_sincos(x, s, c); return c; }
+
+__device__ inline float dm_asin(float x) {
+    const float a = fabsf(x);
+    float z, xx;
+    bool flag = false;
+    if (a > 0.5f) {
+        z = 0.5f * (1.0f - a);
+        xx = sqrtf(z);
+        flag = true;
+    } else {
+        xx = a;
+        z = a * a;
+    }
+    float r;
+    if (a < 1.0e-4f && !flag) {
+        r = xx;
+    } else {
+        r = ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+             1.6666752422e-1f) * z * xx + xx;
+    }
+    if (flag) {
+        r = r + r;
+        r = 1.5707963267948966f - r;
+    }
+    return x < 0.0f ? -r : r;
+}
+__device__ inline float dm_acos(float x) {
+    if (x < -0.5f) return PI_F - 2.0f * dm_asin(sqrtf(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * dm_asin(sqrtf(0.5f * (1.0f - x)));
+    return 1.5707963267948966f - dm_asin(x);
+}
+__device__ inline float dm_atan_core(float x) {
+    float sgn = 1.0f, y;
+    if (x < 0.0f) { sgn = -1.0f; x = -x; }
+    if (x > 2.414213562373095f) {
+        y = 1.5707963267948966f;
+        x = -1.0f / x;
+    } else if (x > 0.4142135623730950f) {
+        y = 0.7853981633974483f;
+        x = (x - 1.0f) / (x + 1.0f);
+    } else {
+        y = 0.0f;
+    }
+    const float z = x * x;
+    y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x + x);
+    return sgn < 0.0f ? -y : y;
+}
+__device__ inline float dm_atan2(float y, float x) {
+    int code = 0;
+    if (x < 0.0f) code = 2;
+    if (y < 0.0f) code |= 1;
+    if (x == 0.0f) {
+        if (code & 1) return -1.5707963267948966f;
+        if (y == 0.0f) return 0.0f;
+        return 1.5707963267948966f;
+    }
+    if (y == 0.0f) return (code & 2) ? PI_F : 0.0f;
+    float w = 0.0f;
+    if (code == 2) w = PI_F;
+    else if (code == 3) w = -PI_F;
+    return w + dm_atan_core(y / x);
+}
+__device__ __forceinline__ float dm_hypot(float x, float y) { return sqrtf(x * x + y * y); }
+
+// ---------------------------------------------------------------------------
+// counter-based RNG
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t path_state(uint32_t seed, uint32_t pixel, uint32_t sample) {
+    uint32_t h = lowbias32(seed ^ 0xA511E9B3u);
+    h = lowbias32(h ^ pixel);
+    return lowbias32(h ^ (sample * 0x9E3779B9u));
+}
+__device__ __forceinline__ float rng_next(uint32_t &st) {
+    const uint32_t s = st * 747796405u + 2891336453u;
+    st = s;
+    uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+    w = (w >> 22u) ^ w;
+    return (float)(w >> 8) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------------------
+// ray / path state
+// ---------------------------------------------------------------------------
+struct PathRay {
+    v3 o, d, n;
+    float col[4];
+    float u, v, t;
+    uint32_t cur, prev, depth, last_prim;
+    bool specular;
+};
+
+struct Esvo {
+    v3 t_coef, t_bias, pos;
+    float t_min, t_max, h, scale_exp2, max_dst;
+    uint32_t parent, pmask, idx, mirror, scale, iter;
+};
+
+struct Counters {
+    uint32_t paths, segs, steps, sph, cub, shade, tex;
+};
+
+__device__ __forceinline__ uint32_t f2u32_sat(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967295.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+
+// Texture::value (texture.rs:64-93), corrected RGBA stride [C9]
+__device__ inline void texture_value(const DevScene &S, uint32_t tex_idx, float u, float v, float out[4],
+                                     Counters &cnt) {
+    const DevTexture t = S.texs[tex_idx];
+    if (t.kind == 0u) {  // F32Color::from(&U8Color) (colors/mod.rs:280-288)
+        out[0] = S.lut_float[t.rgba & 255u];
+        out[1] = S.lut_float[(t.rgba >> 8) & 255u];
+        out[2] = S.lut_float[(t.rgba >> 16) & 255u];
+        out[3] = (float)(t.rgba >> 24) / 255.0f;
+        return;
+    }
+    if (t.height == 0u) { out[0] = out[1] = out[2] = out[3] = 1.0f; return; }
+    float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+    float vv = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+    vv = 1.0f - vv;
+    uint32_t i = f2u32_sat(uu * (float)t.width);
+    uint32_t j = f2u32_sat(vv * (float)t.height);
+    if (i > t.width - 1u) i = t.width - 1u;
+    if (j > t.height - 1u) j = t.height - 1u;
+    const uint32_t px = *reinterpret_cast<const uint32_t *>(S.texels + t.offset + ((uint64_t)j * t.width + i) * 4u);
+    cnt.tex++;
+    out[0] = S.lut_float[px & 255u];
+    out[1] = S.lut_float[(px >> 8) & 255u];
+    out[2] = S.lut_float[(px >> 16) & 255u];
+    out[3] = (float)(px >> 24) / 255.0f;
+}
+
+struct PrimHit {
+    float t;
+    uint32_t inside;
+    uint32_t axis;
+    float nsgn;
+};
+
+// Sphere::hit restated (sphere.rs:33-57) + root selection [C2]
+__device__ __forceinline__ bool sphere_test(float4 sp, const PathRay &r, bool self_prim, PrimHit &h) {
+    const v3 oc = vsub(V(sp.x, sp.y, sp.z), r.o);
+    const float a = vdot(r.d, r.d);
+    const float hh = vdot(r.d, oc);
+    const float cc = vdot(oc, oc) - sp.w * sp.w;
+    const float disc = hh * hh - a * cc;
+    if (disc < 0.0f) return false;
+    const float sq = sqrtf(disc);
+    const float t0 = (hh - sq) / a;
+    const float t1 = (hh + sq) / a;
+    if (self_prim) {
+        if (vdot(r.d, r.n) < 0.0f && t1 > RAY_EPSILON) { h.t = t1; h.inside = 1u; return true; }
+        return false;
+    }
+    if (t0 > RAY_EPSILON) { h.t = t0; h.inside = 0u; return true; }
+    if (t1 > RAY_EPSILON) { h.t = t1; h.inside = 1u; return true; }
+    return false;
+}
+
+__device__ __forceinline__ float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6f : 1.0f / d; }
+
+// AABB::intersects_new (aabb.rs:172-191) [C3]
+__device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const PathRay &r, bool self_prim, PrimHit &h) {
+    const v3 inv = V(inv_clamped(r.d.x), inv_clamped(r.d.y), inv_clamped(r.d.z));
+    const v3 tb = vmul(vsub(V(bmin.x, bmin.y, bmin.z), r.o), inv);
+    const v3 tt = vmul(vsub(V(bmax.x, bmax.y, bmax.z), r.o), inv);
+    const v3 mins = V(fmn(tb.x, tt.x), fmn(tb.y, tt.y), fmn(tb.z, tt.z));
+    const v3 maxs = V(fmx(tb.x, tt.x), fmx(tb.y, tt.y), fmx(tb.z, tt.z));
+    float t0 = vmax3(mins);
+    const float t1 = vmin3(maxs);
+    if (!isfinite(t0)) t0 = t1;
+    if (t1 < t0) return false;
+    uint32_t inside;
+    float t;
+    if (self_prim) {
+        if (!(vdot(r.d, r.n) < 0.0f && t1 > RAY_EPSILON)) return false;
+        inside = 1u; t = t1;
+    } else if (t0 > RAY_EPSILON) {
+        inside = 0u; t = t0;
+    } else if (t1 > RAY_EPSILON) {
+        inside = 1u; t = t1;
+    } else {
+        return false;
+    }
+    uint32_t axis;
+    if (!inside) axis = (mins.x == t0) ? 0u : ((mins.y == t0) ? 1u : 2u);
+    else axis = (maxs.x == t1) ? 0u : ((maxs.y == t1) ? 1u : 2u);
+    const float ia = axis == 0u ? inv.x : (axis == 1u ? inv.y : inv.z);
+    h.nsgn = inside ? (ia > 0.0f ? 1.0f : -1.0f) : (ia > 0.0f ? -1.0f : 1.0f);
+    h.t = t;
+    h.inside = inside;
+    h.axis = axis;
+    return true;
+}
+
+__device__ __forceinline__ uint32_t face_index(uint32_t axis, float sgn) {
+    if (axis == 0u) return sgn < 0.0f ? 0u : 1u;
+    if (axis == 1u) return sgn < 0.0f ? 2u : 3u;
+    return sgn > 0.0f ? 4u : 5u;
+}
+
+// Chunky-style commit [C1]: the ray origin moves to the hit point
+__device__ inline void commit_hit(const DevScene &S, PathRay &r, uint32_t prim, const PrimHit &h, Counters &cnt) {
+    const v3 p = vadd(r.o, vscale(r.d, h.t));
+    float u = 0.0f, v = 0.0f;
+    uint32_t mat;
+    v3 n;
+    bool uv_ready;
+    if (!(prim & kPrimCuboidBit)) {
+        const float4 sp = S.spheres[prim];
+        n = V((p.x - sp.x) / sp.w, (p.y - sp.y) / sp.w, (p.z - sp.z) / sp.w);
+        mat = S.sphere_mat[prim];
+        uv_ready = false;  // sphere uv only feeds image textures (computed lazily below)
+    } else {
+        const uint32_t ci = prim & ~kPrimCuboidBit;
+        const float4 bmin = S.cub_min[ci], bmax = S.cub_max[ci];
+        n = V(0.0f, 0.0f, 0.0f);
+        if (h.axis == 0u) n.x = h.nsgn; else if (h.axis == 1u) n.y = h.nsgn; else n.z = h.nsgn;
+        const float ex = bmax.x - bmin.x, ey = bmax.y - bmin.y, ez = bmax.z - bmin.z;
+        if (h.axis == 0u) {
+            u = (p.z - bmin.z) / ez; v = (p.y - bmin.y) / ey;
+            if (r.d.x < 0.0f) u = 1.0f - u;
+        } else if (h.axis == 1u) {
+            u = (p.x - bmin.x) / ex; v = (p.z - bmin.z) / ez;
+            if (r.d.y < 0.0f) v = 1.0f - v;
+        } else {
+            u = (p.x - bmin.x) / ex; v = (p.y - bmin.y) / ey;
+            if (r.d.z < 0.0f) u = 1.0f - u;
+        }
+        u = fabsf(u);
+        v = fabsf(v);
+        mat = S.cub_mat[6u * ci + face_index(h.axis, h.nsgn)];
+        uv_ready = true;
+    }
+    r.o = p;
+    r.t = h.t;
+    r.n = n;
+    r.last_prim = prim;
+    if (h.inside) {
+        r.cur = 0u;
+        r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;
+    } else {
+        r.cur = mat;
+        const uint32_t tex = S.mats[mat].texture_index;
+        if (!uv_ready && S.texs[tex].kind != 0u) {
+            const float theta = dm_acos(-n.y);  // Sphere::get_uv (sphere.rs:60-69)
+            const float phi = dm_atan2(-n.z, n.x) + PI_F;
+            u = phi / (2.0f * PI_F);
+            v = theta / PI_F;
+        }
+        texture_value(S, tex, u, v, r.col, cnt);
+    }
+    r.u = u;
+    r.v = v;
+}
+
+// ---------------------------------------------------------------------------
+// ESVO (octree_traversal.rs:54-302) split into setup + one iteration
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void stk_write(uint2 *stk, uint32_t slot, uint32_t node, float t) {
+    stk[slot * kBlock] = make_uint2(node, __float_as_uint(t));
+}
+
+__device__ inline void esvo_begin(const DevScene &S, const PathRay &ray, Esvo &E, uint2 *stk) {
+    const float osc = S.octree_scale;
+    for (uint32_t s = 0; s < S.depth; ++s) stk_write(stk, s, 0u, 0.0f);
+    v3 ro = vscale(ray.o, osc);
+    v3 rd = ray.d;
+    E.max_dst = MAX_DST_WORLD * osc;
+    ro = vadd(ro, V(1.0f, 1.0f, 1.0f));
+    E.parent = S.root;
+    E.pmask = S.node_mask[S.root];
+    E.scale = OCTREE_MAX_SCALE - 1u;
+    E.scale_exp2 = 0.5f;
+    const uint32_t epsb = __float_as_uint(OCTREE_EPSILON) & 0x7FFFFFFFu;
+    if (fabsf(rd.x) < OCTREE_EPSILON) rd.x = __uint_as_float(epsb | (__float_as_uint(rd.x) & 0x80000000u));
+    if (fabsf(rd.y) < OCTREE_EPSILON) rd.y = __uint_as_float(epsb | (__float_as_uint(rd.y) & 0x80000000u));
+    if (fabsf(rd.z) < OCTREE_EPSILON) rd.z = __uint_as_float(epsb | (__float_as_uint(rd.z) & 0x80000000u));
+    E.t_coef = V(1.0f / -fabsf(rd.x), 1.0f / -fabsf(rd.y), 1.0f / -fabsf(rd.z));  // [C13]
+    E.t_bias = vmul(E.t_coef, ro);
+    E.mirror = 0u;
+    if (rd.x > 0.0f) { E.mirror |= 1u; E.t_bias.x = 3.0f * E.t_coef.x - E.t_bias.x; }
+    if (rd.y > 0.0f) { E.mirror |= 2u; E.t_bias.y = 3.0f * E.t_coef.y - E.t_bias.y; }
+    if (rd.z > 0.0f) { E.mirror |= 4u; E.t_bias.z = 3.0f * E.t_coef.z - E.t_bias.z; }
+    E.t_min = fmx(vmax3(vsub(vscale(E.t_coef, 2.0f), E.t_bias)), 0.0f);
+    E.t_max = vmin3(vsub(E.t_coef, E.t_bias));
+    E.h = E.t_max;
+    E.idx = 0u;
+    E.pos = V(1.0f, 1.0f, 1.0f);
+    const v3 upper = vsub(vscale(E.t_coef, 1.5f), E.t_bias);
+    if (upper.x > E.t_min) { E.idx ^= 1u; E.pos.x = 1.5f; }
+    if (upper.y > E.t_min) { E.idx ^= 2u; E.pos.y = 1.5f; }
+    if (upper.z > E.t_min) { E.idx ^= 4u; E.pos.z = 1.5f; }
+    E.iter = 0u;
+}
+
+enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
+
+// leaf primitive list test [C1]
+__device__ inline bool leaf_test(const DevScene &S, const PathRay &r, uint32_t leaf, float t_exit_w, float cell_w,
+                                 uint32_t &best_prim, PrimHit &best, Counters &cnt) {
+    const uint2 lr = S.leaf_range[leaf];
+    const float t_accept = t_exit_w + CELL_TOL * cell_w;
+    bool found = false;
+    for (uint32_t k = 0; k < lr.y; ++k) {
+        const uint32_t prim = S.leaf_prims[lr.x + k];
+        const bool self_prim = prim == r.last_prim;
+        PrimHit h;
+        bool ok;
+        if (!(prim & kPrimCuboidBit)) {
+            cnt.sph++;
+            ok = sphere_test(S.spheres[prim], r, self_prim, h);
+        } else {
+            cnt.cub++;
+            const uint32_t ci = prim & ~kPrimCuboidBit;
+            ok = cuboid_test(S.cub_min[ci], S.cub_max[ci], r, self_prim, h);
+        }
+        if (ok && h.t <= t_accept && (!found || h.t < best.t)) {
+            best = h;
+            best_prim = prim;
+            found = true;
+        }
+    }
+    return found;
+}
+
+__device__ inline int esvo_step(const DevScene &S, PathRay &ray, Esvo &E, uint2 *stk, Counters &cnt) {
+    if (E.iter >= OCTREE_MAX_STEPS) return kStepMiss;
+    if (E.max_dst >= 0.0f && E.t_min > E.max_dst) return kStepMiss;
+    E.iter++;
+    cnt.steps++;
+    const v3 t_corner = vsub(vmul(E.pos, E.t_coef), E.t_bias);
+    const float tc_max = vmin3(t_corner);
+    const uint32_t cidx = E.idx ^ E.mirror;
+    const bool present = (E.pmask >> cidx) & 1u;
+    const bool is_leaf = (E.pmask >> (cidx + 8u)) & 1u;
+    if (present && E.t_min <= E.t_max) {
+        if (is_leaf && E.t_min >= 0.0f) {
+            const uint32_t payload = S.node_children[8u * E.parent + cidx];
+            const float cell_w = E.scale_exp2 / S.octree_scale;
+            uint32_t prim;
+            PrimHit h;
+            if (leaf_test(S, ray, payload, tc_max / S.octree_scale, cell_w, prim, h, cnt)) {
+                commit_hit(S, ray, prim, h, cnt);
+                return kStepHit;
+            }
+        } else if (!is_leaf) {
+            const float half = E.scale_exp2 * 0.5f;
+            const v3 t_center = vadd(vscale(E.t_coef, half), t_corner);
+            const float tv_max = fmn(E.t_max, tc_max);
+            if (E.t_min <= tv_max) {
+                const uint32_t child = S.node_children[8u * E.parent + cidx];
+                // validated trees never descend below the leaf level, so the slot is in [0, depth)
+                if (tc_max < E.h && E.scale >= OCTREE_MAX_SCALE - S.depth)
+                    stk_write(stk, E.scale - (OCTREE_MAX_SCALE - S.depth), E.parent, E.t_max);
+                E.h = tc_max;
+                E.parent = child;
+                E.pmask = S.node_mask[child];
+                E.scale -= 1u;
+                E.scale_exp2 = half;
+                E.idx = 0u;
+                if (t_center.x > E.t_min) { E.idx ^= 1u; E.pos.x = E.pos.x + half; }
+                if (t_center.y > E.t_min) { E.idx ^= 2u; E.pos.y = E.pos.y + half; }
+                if (t_center.z > E.t_min) { E.idx ^= 4u; E.pos.z = E.pos.z + half; }
+                E.t_max = tv_max;
+                return kStepContinue;
+            }
+        }
+    }
+    // advance (:249-260)
+    uint32_t step_mask = 0u;
+    if (t_corner.x <= tc_max) { step_mask ^= 1u; E.pos.x = E.pos.x - E.scale_exp2; }
+    if (t_corner.y <= tc_max) { step_mask ^= 2u; E.pos.y = E.pos.y - E.scale_exp2; }
+    if (t_corner.z <= tc_max) { step_mask ^= 4u; E.pos.z = E.pos.z - E.scale_exp2; }
+    E.t_min = tc_max;
+    E.idx ^= step_mask;
+    if ((E.idx & step_mask) != 0u) {  // pop (:262-299)
+        uint32_t diff = 0u;
+        if (step_mask & 1u) diff |= __float_as_uint(E.pos.x) ^ __float_as_uint(E.pos.x + E.scale_exp2);
+        if (step_mask & 2u) diff |= __float_as_uint(E.pos.y) ^ __float_as_uint(E.pos.y + E.scale_exp2);
+        if (step_mask & 4u) diff |= __float_as_uint(E.pos.z) ^ __float_as_uint(E.pos.z + E.scale_exp2);
+        const uint32_t scale = diff ? 31u - (uint32_t)__clz(diff) : 0xFFFFFFFFu;
+        if (scale >= OCTREE_MAX_SCALE) return kStepMiss;
+        E.scale = scale;
+        E.scale_exp2 = __uint_as_float((scale - OCTREE_MAX_SCALE + 127u) << 23);
+        // slots below the finest level were never written: the oracle reads its zeroed entry
+        const uint32_t base = OCTREE_MAX_SCALE - S.depth;
+        uint2 e = make_uint2(0u, 0u);
+        if (scale >= base) e = stk[(scale - base) * kBlock];
+        E.parent = e.x;
+        E.pmask = S.node_mask[e.x];
+        E.t_max = __uint_as_float(e.y);
+        const uint32_t shx = __float_as_uint(E.pos.x) >> scale;
+        const uint32_t shy = __float_as_uint(E.pos.y) >> scale;
+        const uint32_t shz = __float_as_uint(E.pos.z) >> scale;
+        E.pos = V(__uint_as_float(shx << scale), __uint_as_float(shy << scale), __uint_as_float(shz << scale));
+        E.idx = (shx & 1u) | ((shy & 1u) << 1) | ((shz & 1u) << 2);
+        E.h = 0.0f;
+    }
+    return kStepContinue;
+}
+
+// next_intersection prologue (path_tracer.rs:438-446) + Scene::hit direction guard (scene/mod.rs:175-179)
+__device__ __forceinline__ void begin_segment(const DevScene &S, PathRay &ray, Esvo &E, uint2 *stk) {
+    ray.prev = ray.cur;
+    const v3 d = ray.d;
+    if ((d.x == 0.0f && d.y == 0.0f && d.z == 0.0f) || isnan(d.x) || isnan(d.y) || isnan(d.z))
+        ray.d = V(0.0f, 1.0f, 0.0f);
+    esvo_begin(S, ray, E, stk);
+}
+
+// ---------------------------------------------------------------------------
+// sky + sun (scene/mod.rs:216-268, 384-426)
+// ---------------------------------------------------------------------------
+__device__ inline void sky_color(const DevSun &K, const PathRay &r, float out[3]) {
+    out[0] = 0.5f; out[1] = 0.7f; out[2] = 1.0f;
+    const v3 d = r.d;
+    const bool textured = (r.depth == 0u) || r.specular;  // get_sky_color_interp / get_sky_color(true)
+    if (textured ? !K.draw_texture : !K.diffuse_sun) return;
+    if (vdot(d, V(K.sw[0], K.sw[1], K.sw[2])) < 0.5f) return;
+    const float a = PI_F / 2.0f - dm_acos(vdot(d, V(K.su[0], K.su[1], K.su[2]))) + K.width;
+    if (!(a >= 0.0f && a < K.width2)) return;
+    const float b = PI_F / 2.0f - dm_acos(vdot(d, V(K.sv[0], K.sv[1], K.sv[2]))) + K.width;
+    if (!(b >= 0.0f && b < K.width2)) return;
+    if (textured) {
+        for (int i = 0; i < 3; ++i) out[i] = K.tex[i] * K.isect_mul[i] + out[i];
+    } else {
+        for (int i = 0; i < 3; ++i) out[i] = (K.tex[i] * K.diffuse_mul[i]) * K.luminosity + out[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// scatter kernels (ray/mod.rs:113-373), in place: `r` becomes the next ray
+// ---------------------------------------------------------------------------
+__device__ inline void specular_reflection(PathRay &r, float roughness, uint32_t &rng) {
+    const v3 n = r.n, dir = r.d;
+    r.u = r.v = 0.0f;
+    r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;
+    r.cur = r.prev;
+    if (roughness > RAY_EPSILON) {
+        const float sdot = -2.0f * vdot(dir, n);
+        const v3 spec = vadd(vscale(n, sdot), dir);
+        const float x1 = rng_next(rng), x2 = rng_next(rng);
+        const float rr = sqrtf(x1), theta = 2.0f * PI_F * x2;
+        float sn, cs;
+        dm_sincos(theta, sn, cs);
+        const float tx = rr * cs, ty = rr * sn, tz = sqrtf(1.0f - x1);
+        const v3 tangent = fabsf(n.x) > 0.1f ? V(0.0f, 1.0f, 0.0f) : V(1.0f, 0.0f, 0.0f);
+        const v3 u = vnorm(vcross(tangent, n));
+        const v3 v = vcross(n, u);
+        const v3 nd = vadd(vadd(vscale(u, tx), vscale(v, ty)), vscale(n, tz));
+        r.d = vnorm(vadd(vscale(nd, roughness), vscale(spec, 1.0f - roughness)));
+    } else {
+        r.d = vsub(dir, vscale(n, 2.0f * vdot(dir, n)));
+    }
+    r.o = vadd(r.o, vscale(r.d, RAY_OFFSET));
+    if (signum_(vdot(n, r.d)) == signum_(vdot(n, dir))) {
+        const float factor = vdot(n, dir) * -RAY_EPSILON - vdot(r.d, n);
+        r.d = vnorm(vadd(r.d, vscale(n, factor)));
+    }
+}
+
+__device__ inline void diffuse_reflection(const DevSun &K, PathRay &r, uint32_t &rng) {
+    const v3 n = r.n;
+    const v3 d_in = r.d;
+    r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;  // new_from_self
+    float x1 = rng_next(rng), x2 = rng_next(rng);
+    float rr = sqrtf(x1), theta = 2.0f * PI_F * x2;
+    float sn, cs;
+    dm_sincos(theta, sn, cs);
+    float tx = rr * cs, ty = rr * sn;
+    if (K.importance_sampling) {
+        const float sdx = K.sun_dx, sdy = K.sun_dy, sdz = K.sun_dz;
+        float stx, sty, sq;
+        const float stz = (sdx * n.x + sdy * n.y) + sdz * n.z;
+        if (fabsf(n.x) > 0.1f) {
+            stx = sdx * n.z - sdz * n.x;
+            sty = (sdx * n.x * n.y - sdy * (n.x * n.x + n.z * n.z)) + sdz * n.y * n.z;
+            sq = dm_hypot(n.x, n.z);
+        } else {
+            stx = sdz * n.y - sdy * n.z;
+            sty = (sdy * n.x * n.y - sdx * (n.y * n.y + n.z * n.z)) + sdz * n.x * n.z;
+            sq = dm_hypot(n.z, n.y);
+        }
+        stx /= sq;
+        sty /= sq;
+        const float cr = K.circle_radius;
+        float chance = K.sample_chance;
+        const float alt_rel = dm_asin(stz);
+        if (alt_rel + cr > RAY_EPSILON) {
+            if ((dm_hypot(stx, sty) + cr) + RAY_EPSILON < 1.0f) {
+                if (rng_next(rng) < chance) {
+                    tx = stx + tx * cr;
+                    ty = sty + ty * cr;
+                } else {
+                    while (dm_hypot(tx - stx, ty - sty) < cr) {
+                        tx -= stx;
+                        ty -= sty;
+                        if (tx == 0.0f && ty == 0.0f) break;
+                        tx /= cr;
+                        ty /= cr;
+                    }
+                }
+            } else {
+                const float min_r = dm_cos(alt_rel + cr);
+                const float max_r = dm_cos(fmx(alt_rel - cr, 0.0f));
+                const float sun_theta = dm_atan2(sty, stx);
+                const float seg = ((max_r * max_r - min_r * min_r) * cr) / PI_F;
+                chance *= seg / (cr * cr);
+                chance = fmn(chance, SUN_MAX_CHANCE);
+                if (rng_next(rng) < chance) {
+                    rr = sqrtf(min_r * min_r * x1 + max_r * max_r * (1.0f - x1));
+                    theta = sun_theta + (2.0f * x2 - 1.0f) * cr;
+                } else {
+                    for (;;) {
+                        if (!(rr > min_r && rr < max_r)) break;
+                        float diff = fabsf(theta - sun_theta);
+                        if (diff >= 2.0f * PI_F) diff = diff - 2.0f * PI_F;
+                        const float ad = diff > PI_F ? 2.0f * PI_F - diff : diff;
+                        if (!(ad < cr)) break;
+                        x1 = rng_next(rng);
+                        x2 = rng_next(rng);
+                        rr = sqrtf(x1);
+                        theta = 2.0f * PI_F * x2;
+                    }
+                }
+                dm_sincos(theta, sn, cs);
+                tx = rr * cs;
+                ty = rr * sn;
+            }
+        }
+    }
+    const float tz = sqrtf((1.0f - tx * tx) - ty * ty);
+    float xx, xy, xz;
+    if (fabsf(n.x) > 0.1f) { xx = 0.0f; xy = 1.0f; xz = 0.0f; } else { xx = 1.0f; xy = 0.0f; xz = 0.0f; }
+    float ux = xy * n.z - xz * n.y, uy = xz * n.x - xx * n.z, uz = xx * n.y - xy * n.x;
+    const float inv = 1.0f / sqrtf((ux * ux + uy * uy) + uz * uz);
+    ux *= inv; uy *= inv; uz *= inv;
+    const float vx = uy * n.z - uz * n.y, vy = uz * n.x - ux * n.z, vz = ux * n.y - uy * n.x;
+    r.d = V((ux * tx + vx * ty) + n.x * tz, (uy * tx + vy * ty) + n.y * tz, (uz * tx + vz * ty) + n.z * tz);
+    r.o = vadd(r.o, vscale(r.d, RAY_OFFSET));
+    r.cur = r.prev;
+    r.specular = false;
+    if (signum_(vdot(n, r.d)) == signum_(vdot(n, d_in))) {
+        const float factor = signum_(vdot(n, d_in)) * -RAY_EPSILON - vdot(r.d, n);
+        r.d = vnorm(vadd(r.d, vscale(n, factor)));
+    }
+}
+
+enum : uint32_t { ST_IDLE = 0, ST_NEWPATH, ST_BEGIN, ST_TRAV, ST_HIT, ST_MISS, ST_FINISH, ST_DONE };
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ void item_pixel(const DevRender &R, uint32_t item, uint32_t &x, uint32_t &y) {
+    const uint32_t lt = item >> 6, w = item & 63u;
+    const uint32_t t = R.shard_index + lt * R.shard_count;
+    x = (t % R.tiles_x) * kTile + (w & 7u);
+    y = (t / R.tiles_x) * kTile + (w >> 3);
+}
+
+__device__ inline unsigned long long wave_sum(uint32_t v) {
+    unsigned long long s = v;
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    return s;
+}
+
+__global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C, DevRender R, float4 *__restrict__ accum,
+                                                        uint32_t *__restrict__ segcount, uint32_t *__restrict__ counter,
+                                                        unsigned long long *__restrict__ stats) {
+    extern __shared__ uint2 lds_stack[];
+    uint2 *stk = lds_stack + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const v3 cam_eye = V(C.eye[0], C.eye[1], C.eye[2]);
+    const v3 cam_dir = V(C.dir[0], C.dir[1], C.dir[2]);
+    const v3 cam_right = V(C.right[0], C.right[1], C.right[2]);
+    const v3 cam_up = V(C.up[0], C.up[1], C.up[2]);
+    const float jlo = -1.0f / R.dim, jhi = 1.0f / R.dim;
+
+    uint32_t state = ST_IDLE;
+    uint32_t item = 0u, pix = 0u, k = 0u, pix_segs = 0u, path_segs = 0u, acc_idx = 0u;
+    float4 fb = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    PathRay ray;
+    ray.cur = ray.prev = ray.depth = 0u;
+    ray.last_prim = kPrimNone;
+    ray.specular = true;
+    v3 T = V(1.0f, 1.0f, 1.0f), L = V(0.0f, 0.0f, 0.0f);
+    uint32_t rng = 0u;
+    Esvo E;
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+
+    for (;;) {
+        // --- refill: lanes without a pixel take the next work items (one atomic per wave)
+        const uint64_t need = __ballot(state == ST_IDLE);
+        if (need) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need) - 1u;
+            uint32_t base = 0u;
+            if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(need));
+            base = __shfl(base, (int)leader);
+            if (state == ST_IDLE) {
+                const uint32_t my = base + lanes_below(need);
+                if (my >= R.total_items) {
+                    state = ST_DONE;
+                } else {
+                    uint32_t x, y;
+                    item_pixel(R, my, x, y);
+                    if (x < R.W && y < R.H) {
+                        item = my;
+                        pix = y * R.W + x;
+                        acc_idx = R.compact ? item : pix;
+                        fb = accum[acc_idx];
+                        k = 0u;
+                        pix_segs = 0u;
+                        state = ST_NEWPATH;
+                    }
+                }
+            }
+        }
+        if (__ballot(state != ST_DONE) == 0ull) break;
+
+        // --- camera ray (camera.rs:77-86, tile_renderer.rs:695-703)
+        if (state == ST_NEWPATH) {
+            const uint32_t x = pix % R.W, y = pix / R.W;
+            rng = path_state(R.seed, pix, R.spp_start + k);
+            const float xn = ((float)(2u * x + 1u) - (float)R.W) / R.dim;
+            const float yn = ((float)(2u * (R.H - y) - 1u) - (float)R.H) / R.dim;
+            const float dx = jlo + (jhi - jlo) * rng_next(rng);
+            const float dy = jlo + (jhi - jlo) * rng_next(rng);
+            const v3 nd = vadd(vadd(vscale(cam_dir, C.d_factor), vscale(cam_right, xn + dx)), vscale(cam_up, yn + dy));
+            ray.o = cam_eye;
+            ray.d = vnorm(nd);
+            ray.n = V(0.0f, 0.0f, 0.0f);
+            ray.cur = ray.prev = ray.depth = 0u;
+            ray.last_prim = kPrimNone;
+            ray.specular = true;
+            T = V(1.0f, 1.0f, 1.0f);
+            L = V(0.0f, 0.0f, 0.0f);
+            path_segs = 0u;
+            cnt.paths++;
+            state = ST_BEGIN;
+        }
+        if (state == ST_BEGIN) {
+            if (path_segs >= MAX_PATH_SEGMENTS) {
+                state = ST_FINISH;  // [C15]: the path ends without further contribution
+            } else {
+                begin_segment(S, ray, E, stk);
+                cnt.segs++;
+                pix_segs++;
+                path_segs++;
+                state = ST_TRAV;
+            }
+        }
+
+        // --- traversal: keep stepping while at least half of the live lanes traverse
+        {
+            bool first = true;
+            for (;;) {
+                const uint64_t tm = __ballot(state == ST_TRAV);
+                if (tm == 0ull) break;
+                if (!first) {
+                    const uint64_t am = __ballot(state != ST_DONE);
+                    if (2u * (uint32_t)__popcll(tm) < (uint32_t)__popcll(am)) break;
+                }
+                first = false;
+                if (state == ST_TRAV) {
+                    const int rs = esvo_step(S, ray, E, stk, cnt);
+                    if (rs == kStepHit) state = ST_HIT;
+                    else if (rs == kStepMiss) state = ST_MISS;
+                }
+            }
+        }
+
+        // --- shading (path_tracer.rs:15-135 in forward-throughput form)
+        if (state == ST_HIT || state == ST_MISS || state == ST_FINISH) {
+            bool path_done = state == ST_FINISH;
+            if (state == ST_MISS) {
+                float sky[3];
+                sky_color(S.sun, ray, sky);
+                L = V(L.x + T.x * sky[0], L.y + T.y * sky[1], L.z + T.z * sky[2]);
+                path_done = true;
+            } else if (state == ST_HIT) {
+                const DevMaterial m = S.mats[ray.cur];
+                const float ior2 = S.mats[ray.prev].ior;
+                const float specular = m.specular, diffuse = ray.col[3], absorb = ray.col[3];
+                const float ior1 = m.ior;
+                if (ray.col[3] + specular < RAY_EPSILON && ior1 == ior2) {  // [C4]
+                    ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
+                    state = ST_BEGIN;
+                } else if (ray.depth + 1u >= R.max_depth) {
+                    path_done = true;
+                } else {
+                    ray.depth += 1u;
+                    cnt.shade++;
+                    const float metal = m.metalness;
+                    const bool do_metal = metal > RAY_EPSILON && rng_next(rng) < metal;
+                    if (do_metal || (specular > RAY_EPSILON && rng_next(rng) < specular)) {
+                        if (do_metal) T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
+                        specular_reflection(ray, m.roughness, rng);
+                    } else if (rng_next(rng) < diffuse) {
+                        if (S.emitters && m.emittance > RAY_EPSILON) {
+                            const v3 e = V(ray.col[0] * ray.col[0] * m.emittance, ray.col[1] * ray.col[1] * m.emittance,
+                                           ray.col[2] * ray.col[2] * m.emittance);
+                            L = V(L.x + T.x * e.x, L.y + T.y * e.y, L.z + T.z * e.z);
+                        }
+                        T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
+                        diffuse_reflection(S.sun, ray, rng);
+                    } else if (fabsf(ior1 - ior2) >= RAY_EPSILON) {
+                        // do_refraction (path_tracer.rs:318-401) [C14]
+                        const bool refr = (m.flags & MAT_FLAG_REFRACTIVE) != 0u;
+                        const float n1n2 = ior1 / ior2;
+                        const float cos_theta = -vdot(ray.d, ray.n);
+                        const float radicand = 1.0f - n1n2 * n1n2 * (1.0f - cos_theta * cos_theta);
+                        if (refr && radicand < RAY_EPSILON) {
+                            specular_reflection(ray, m.roughness, rng);
+                        } else {
+                            const float a = n1n2 - 1.0f, b = n1n2 + 1.0f;
+                            const float r0 = a * a / (b * b);
+                            const float cc = 1.0f - cos_theta;
+                            const float c5 = ((cc * cc) * (cc * cc)) * cc;
+                            const float rtheta = r0 + (1.0f - r0) * c5;
+                            if (rng_next(rng) < rtheta) {
+                                specular_reflection(ray, m.roughness, rng);
+                            } else {
+                                T = V(T.x * (ray.col[0] * absorb), T.y * (ray.col[1] * absorb), T.z * (ray.col[2] * absorb));
+                                const v3 d_in = ray.d, n = ray.n;
+                                ray.col[0] = ray.col[1] = ray.col[2] = ray.col[3] = 0.0f;
+                                if (refr) {
+                                    const float t2 = sqrtf(radicand);
+                                    v3 d;
+                                    if (cos_theta > 0.0f) d = vadd(vscale(d_in, n1n2), vscale(n, n1n2 * cos_theta - t2));
+                                    else d = vsub(vscale(d_in, n1n2), vscale(n, -n1n2 * cos_theta - t2));
+                                    ray.d = vnorm(d);
+                                    if (signum_(vdot(n, ray.d)) != signum_(vdot(n, d_in))) {
+                                        const float factor = signum_(vdot(n, d_in)) * -RAY_EPSILON - vdot(ray.d, n);
+                                        ray.d = vnorm(vadd(ray.d, vscale(n, factor)));
+                                    }
+                                    ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
+                                }
+                            }
+                        }
+                    } else {
+                        // do_transmission (path_tracer.rs:403-422)
+                        T = V(T.x * (ray.col[0] * absorb), T.y * (ray.col[1] * absorb), T.z * (ray.col[2] * absorb));
+                        ray.col[0] = ray.col[1] = ray.col[2] = ray.col[3] = 0.0f;
+                        ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
+                    }
+                    state = ST_BEGIN;
+                }
+            }
+            if (path_done) {
+                // running mean of render_tile_average (tile_renderer.rs:716-733), branch_count = 1
+                const uint32_t spp = R.spp_start + k;
+                const float s_inv = 1.0f / (float)(1u + spp);
+                const float fs = (float)spp;
+                fb.x = (fb.x * fs + L.x * 1.0f) * s_inv;
+                fb.y = (fb.y * fs + L.y * 1.0f) * s_inv;
+                fb.z = (fb.z * fs + L.z * 1.0f) * s_inv;
+                k++;
+                if (k < R.spp_count) {
+                    state = ST_NEWPATH;
+                } else {
+                    accum[acc_idx] = fb;
+                    if (segcount) segcount[acc_idx] += pix_segs;
+                    state = ST_IDLE;
+                }
+            }
+        }
+    }
+
+    // --- statistics: one 64-bit atomic per counter per wave
+    const uint32_t vals[kStatCount] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};
+#pragma unroll
+    for (int i = 0; i < kStatCount; ++i) {
+        const unsigned long long s = wave_sum(vals[i]);
+        if (lane == 0u && s) atomicAdd(&stats[i], s);
+    }
+}
+
+// one ray per thread closest-hit query (Scene::hit) for octpt_intersect
+__global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const float *__restrict__ rays,
+                                                           const uint32_t *__restrict__ last_prim,
+                                                           const float *__restrict__ last_normal, uint32_t n,
+                                                           float *__restrict__ out_t, uint32_t *__restrict__ out_prim,
+                                                           float *__restrict__ out_normal, uint32_t *__restrict__ out_steps) {
+    extern __shared__ uint2 lds_stack[];
+    uint2 *stk = lds_stack + threadIdx.x;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    PathRay ray;
+    ray.o = V(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+    ray.d = V(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+    ray.n = last_normal ? V(last_normal[3 * i], last_normal[3 * i + 1], last_normal[3 * i + 2]) : V(0.0f, 0.0f, 0.0f);
+    ray.cur = ray.prev = ray.depth = 0u;
+    ray.last_prim = last_prim ? last_prim[i] : kPrimNone;
+    ray.specular = true;
+    Esvo E;
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    esvo_begin(S, ray, E, stk);
+    int rs;
+    do {
+        rs = esvo_step(S, ray, E, stk, cnt);
+    } while (rs == kStepContinue);
+    if (rs == kStepHit) {
+        out_t[i] = ray.t;
+        out_prim[i] = ray.last_prim;
+        if (out_normal) {
+            out_normal[3 * i] = ray.n.x;
+            out_normal[3 * i + 1] = ray.n.y;
+            out_normal[3 * i + 2] = ray.n.z;
+        }
+    } else {
+        out_t[i] = __int_as_float(0x7f800000);
+        out_prim[i] = kPrimNone;
+        if (out_normal) out_normal[3 * i] = out_normal[3 * i + 1] = out_normal[3 * i + 2] = 0.0f;
+    }
+    if (out_steps) out_steps[i] = E.iter;
+}
+
+__global__ void tonemap_kernel(const float4 *__restrict__ accum, uchar4 *__restrict__ out, uint32_t n,
+                               const uint8_t *__restrict__ lut) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 c = accum[i];
+    const float r = fminf(c.x * 255.0f, 255.0f), g = fminf(c.y * 255.0f, 255.0f), b = fminf(c.z * 255.0f, 255.0f),
+                a = fminf(c.w * 255.0f, 255.0f);
+    out[i] = make_uchar4(lut[f2u32_sat(r)], lut[f2u32_sat(g)], lut[f2u32_sat(b)], (uint8_t)f2u32_sat(a));
+}
+
+__global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t N, const float4 *__restrict__ shards, uint32_t stride,
+                               float4 *__restrict__ frame) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W * H) return;
+    const uint32_t x = i % W, y = i / W;
+    const uint32_t tiles_x = (W + kTile - 1u) / kTile;
+    const uint32_t t = (y / kTile) * tiles_x + x / kTile;
+    const uint32_t shard = t % N, lt = t / N;
+    frame[i] = shards[(size_t)shard * stride + (size_t)lt * 64u + (y % kTile) * kTile + (x % kTile)];
+}
+
+}  // namespace
+
+size_t render_lds_bytes(uint32_t depth) { return (size_t)depth * kBlock * sizeof(uint2); }
+
+int render_blocks_per_cu(uint32_t depth) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void *>(render_kernel), kBlock,
+                                                     render_lds_bytes(depth)) != hipSuccess)
+        return 1;
+    return blocks > 0 ? blocks : 1;
+}
+
+hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum, uint32_t *segcount,
+                         uint32_t *counter, unsigned long long *stats, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R, accum,
+                       segcount, counter, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t *last_prim, const float *last_normal,
+                            uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps, hipStream_t stream) {
+    const uint32_t grid = (n + kBlock - 1u) / kBlock;
+    hipLaunchKernelGGL(intersect_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, rays,
+                       last_prim, last_normal, n, t, prim, normal, steps);
+    return hipGetLastError();
+}
+
+hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const uint8_t *lut_byte, hipStream_t stream) {
+    hipLaunchKernelGGL(tonemap_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, accum, out, n, lut_byte);
+    return hipGetLastError();
+}
+
+hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards, uint32_t stride,
+                          float4 *frame, hipStream_t stream) {
+    hipLaunchKernelGGL(unshard_kernel, dim3((W * H + 255u) / 256u), dim3(256), 0, stream, W, H, shard_count, shards,
+                       stride, frame);
+    return hipGetLastError();
+}
+
+}  // namespace octpt

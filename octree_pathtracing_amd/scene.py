@@ -1,0 +1,429 @@
+"""Scene model mirroring the reference's Scene / Octree / Material / Texture / Sun / Camera
+(reference src/scene/mod.rs:146-156, src/octree/new_octree.rs:13-74,
+src/textures/material.rs:185-195, src/textures/texture.rs:15-18, src/scene/mod.rs:271-383,
+src/renderer/camera.rs:8-66), plus the seeded synthetic scene generator of BASELINE.json's
+configs C1-C5.  All arrays are numpy; the octree is built by the product's
+C++ builder (``liboctpt.so: octpt_build_octree``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib
+
+F32 = np.float32
+PI = F32(np.pi)  # std::f32::consts::PI
+
+# MaterialFlags (material.rs:99-108)
+OPAQUE, SUBSURFACE_SCATTER, REFRACTIVE, WATERLOGGED, SOLID = 0x1, 0x2, 0x4, 0x8, 0x10
+DEFAULT_IOR = F32(1.000293)
+
+
+@dataclass
+class Material:
+    """GPUMaterial field set (gpu_material.rs:67-76); defaults = MaterialBuilder::build."""
+    ior: float = float(DEFAULT_IOR)
+    specular: float = 0.0
+    emittance: float = 0.0
+    roughness: float = 0.0
+    metalness: float = 0.0
+    texture_index: int = 0
+    tint_index: int = 0
+    flags: int = OPAQUE | SOLID
+
+
+def air_material(texture_index: int = 0) -> Material:
+    """Material::AIR (material.rs:198-207)."""
+    return Material(ior=float(DEFAULT_IOR), flags=0, texture_index=texture_index)
+
+
+@dataclass
+class Texture:
+    """Texture::Color(U8Color) or Texture::Image(RTWImage as RGBA8)."""
+    kind: int = _lib.TEXTURE_COLOR
+    rgba: tuple = (255, 0, 255, 255)  # Texture::DEFAULT_TEXTURE (texture.rs:49)
+    pixels: np.ndarray | None = None  # (h, w, 4) uint8 for images
+
+    @staticmethod
+    def color(r: int, g: int, b: int, a: int = 255) -> "Texture":
+        return Texture(_lib.TEXTURE_COLOR, (r, g, b, a), None)
+
+    @staticmethod
+    def image(rgba: np.ndarray) -> "Texture":
+        rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+        assert rgba.ndim == 3 and rgba.shape[2] == 4
+        return Texture(_lib.TEXTURE_IMAGE, (0, 0, 0, 0), rgba)
+
+
+@dataclass
+class SunSamplingStrategy:
+    """SunSamplingStrategy presets (scene/mod.rs:77-127)."""
+    sun_sampling: bool = False
+    diffuse_sun: bool = True
+    strict_direct_light: bool = False
+    sun_luminosity: bool = True
+    importance_sampling: bool = True
+
+
+STRATEGY_OFF = SunSamplingStrategy(False, True, False, True, False)
+STRATEGY_NON_LUMINOUS = SunSamplingStrategy(False, False, False, False, False)
+STRATEGY_FAST = SunSamplingStrategy(True, False, False, False, False)
+STRATEGY_IMPORTANCE = SunSamplingStrategy(False, True, False, True, True)
+STRATEGY_HIGH_QUALITY = SunSamplingStrategy(True, True, True, True, False)
+
+
+@dataclass
+class Sun:
+    """Sun::default (scene/mod.rs:294-307) arguments + tunables."""
+    azimuth: float = float(PI / F32(2.5))
+    altitude: float = float(PI / F32(3.0))
+    radius: float = 0.03
+    color: tuple = (1.0, 1.0, 1.0, 1.0)
+    texture_rgba: tuple = (255, 255, 255, 255)
+    draw_texture: bool = True
+    texture_modification: bool = False
+    apparent_color: tuple = (1.0, 1.0, 1.0)
+    importance_sample_chance: float = 0.1
+    importance_sample_radius: float = 1.2
+    luminosity: float = 100.0
+
+
+@dataclass
+class Camera:
+    """renderer::camera::Camera (camera.rs:8-39); default eye (0,0,10), dir +Z, up +Y, fov 70 deg."""
+    eye: tuple = (0.0, 0.0, 10.0)
+    direction: tuple = (0.0, 0.0, 1.0)
+    up: tuple = (0.0, 1.0, 0.0)
+    fov: float = float(F32(70.0) * (PI / F32(180.0)))  # 70f32.to_radians()
+
+    @staticmethod
+    def look_at(eye, center, up=(0.0, 1.0, 0.0), fov=None) -> "Camera":
+        """Camera::look_at (camera.rs:53-66), evaluated in f32."""
+        eye = np.asarray(eye, F32)
+        center = np.asarray(center, F32)
+        up = np.asarray(up, F32)
+        d = center - eye
+        d = d * (F32(1.0) / np.sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]))
+        k = (up[0] * d[0] + up[1] * d[1]) + up[2] * d[2]
+        u = up - k * d
+        u = u * (F32(1.0) / np.sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]))
+        cam = Camera(tuple(map(float, eye)), tuple(map(float, d)), tuple(map(float, u)))
+        if fov is not None:
+            cam.fov = float(fov)
+        return cam
+
+
+@dataclass
+class Octree:
+    """new_octree::Octree (new_octree.rs:13-19) + leaf payload -> primitive lists."""
+    octant_mask: np.ndarray      # uint16 [n]
+    octant_children: np.ndarray  # uint32 [n, 8]
+    root: int
+    depth: int
+    leaf_first: np.ndarray       # uint32 [leaves]
+    leaf_count: np.ndarray       # uint32 [leaves]
+    leaf_prims: np.ndarray       # uint32 [sum(count)]
+
+    @property
+    def scale(self) -> float:
+        """Octree::scale (new_octree.rs:40-42)."""
+        return float(np.exp2(-float(self.depth)))
+
+    @property
+    def octant_count(self) -> int:
+        return int(self.octant_mask.shape[0])
+
+    @staticmethod
+    def empty(depth: int) -> "Octree":
+        return Octree(np.zeros(1, np.uint16), np.zeros((1, 8), np.uint32), 0, depth,
+                      np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+
+    def octants_struct(self):
+        arr = (_lib.Octant * self.octant_count)()
+        buf = np.frombuffer(arr, dtype=np.dtype([("m", "<u2"), ("r", "<u2"), ("c", "<u4", (8,))]))
+        buf["m"] = self.octant_mask
+        buf["r"] = 0
+        buf["c"] = self.octant_children
+        return arr
+
+
+@dataclass
+class Scene:
+    """scene::Scene (scene/mod.rs:146-156) with a primitive world in place of quads."""
+    spheres: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), F32))          # cx, cy, cz, r
+    sphere_material: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    cuboids: np.ndarray = field(default_factory=lambda: np.zeros((0, 6), F32))          # min xyz, max xyz
+    cuboid_material: np.ndarray = field(default_factory=lambda: np.zeros((0, 6), np.uint32))
+    materials: list = field(default_factory=lambda: [air_material()])
+    textures: list = field(default_factory=lambda: [Texture()])
+    sun: Sun = field(default_factory=Sun)
+    strategy: SunSamplingStrategy = field(default_factory=lambda: STRATEGY_IMPORTANCE)
+    emitters_enabled: bool = True
+    octree: Octree | None = None
+
+    # ---------------------------------------------------------------- octree
+    def build_octree(self, depth: int) -> Octree:
+        """Voxelise the primitives with the product builder (octpt_build_octree)."""
+        lib = _lib.load()
+        sph = self.sphere_structs()
+        cub = self.cuboid_structs()
+        handle = C.c_void_p()
+        st = lib.octpt_build_octree(C.cast(sph, C.c_void_p) if len(self.spheres) else None, len(self.spheres),
+                                    C.cast(cub, C.c_void_p) if len(self.cuboids) else None, len(self.cuboids),
+                                    depth, C.byref(handle))
+        _lib.check(lib, None, st)
+        try:
+            v = _lib.OctreeView()
+            _lib.check(lib, None, lib.octpt_octree_get_view(handle, C.byref(v)))
+            dt = np.dtype([("m", "<u2"), ("r", "<u2"), ("c", "<u4", (8,))])
+            oct_ = np.frombuffer(C.string_at(v.octants, 36 * v.octant_count), dtype=dt)
+
+            def u32(ptr, n):
+                return np.frombuffer(C.string_at(ptr, 4 * n), dtype=np.uint32).copy() if n else np.zeros(0, np.uint32)
+
+            self.octree = Octree(oct_["m"].copy(), oct_["c"].copy(), int(v.root), int(v.depth),
+                                 u32(v.leaf_first, v.leaf_table_size), u32(v.leaf_count, v.leaf_table_size),
+                                 u32(v.leaf_prims, v.leaf_prim_count))
+        finally:
+            lib.octpt_octree_free(handle)
+        return self.octree
+
+    # ---------------------------------------------------------------- ABI views
+    def sphere_structs(self):
+        n = len(self.spheres)
+        arr = (_lib.Sphere * max(n, 1))()
+        if n:
+            buf = np.frombuffer(arr, dtype=np.dtype([("c", "<f4", (3,)), ("r", "<f4"), ("m", "<u4"), ("p", "<u4", (3,))]))
+            buf["c"][:n] = self.spheres[:, :3]
+            buf["r"][:n] = self.spheres[:, 3]
+            buf["m"][:n] = self.sphere_material
+        return arr
+
+    def cuboid_structs(self):
+        n = len(self.cuboids)
+        arr = (_lib.Cuboid * max(n, 1))()
+        if n:
+            buf = np.frombuffer(arr, dtype=np.dtype([("lo", "<f4", (3,)), ("hi", "<f4", (3,)), ("m", "<u4", (6,))]))
+            buf["lo"][:n] = self.cuboids[:, :3]
+            buf["hi"][:n] = self.cuboids[:, 3:]
+            buf["m"][:n] = self.cuboid_material
+        return arr
+
+    def sun_struct(self) -> "_lib.Sun":
+        s = self.sun
+        st = self.strategy
+        return _lib.Sun(s.azimuth, s.altitude, s.radius, (C.c_float * 4)(*s.color), (C.c_float * 3)(*s.apparent_color),
+                        int(s.draw_texture), int(s.texture_modification), s.importance_sample_chance,
+                        s.importance_sample_radius, s.luminosity, (C.c_uint8 * 4)(*s.texture_rgba),
+                        int(st.importance_sampling), int(st.diffuse_sun), int(st.sun_sampling))
+
+    def to_desc(self):
+        """octpt_scene_desc for octpt_scene_upload; returns (desc, keepalive)."""
+        if self.octree is None:
+            raise ValueError("scene has no octree: call build_octree(depth) first")
+        t = self.octree
+        keep = []
+
+        def ptr(a):
+            if a is None or (hasattr(a, "__len__") and len(a) == 0):
+                return None
+            keep.append(a)
+            if isinstance(a, np.ndarray):
+                return a.ctypes.data_as(C.c_void_p)
+            return C.cast(a, C.c_void_p)
+
+        octs = t.octants_struct()
+        lf = np.ascontiguousarray(t.leaf_first, np.uint32)
+        lc = np.ascontiguousarray(t.leaf_count, np.uint32)
+        lp = np.ascontiguousarray(t.leaf_prims, np.uint32)
+        mats = (_lib.Material * len(self.materials))(*[
+            _lib.Material(m.ior, m.specular, m.emittance, m.roughness, m.metalness, m.texture_index, m.tint_index, m.flags)
+            for m in self.materials])
+        texs = (_lib.Texture * len(self.textures))()
+        for i, tx in enumerate(self.textures):
+            texs[i].kind = tx.kind
+            texs[i].rgba[:] = list(tx.rgba)
+            if tx.kind == _lib.TEXTURE_IMAGE:
+                px = np.ascontiguousarray(tx.pixels, np.uint8)
+                keep.append(px)
+                texs[i].width, texs[i].height = px.shape[1], px.shape[0]
+                texs[i].pixels = px.ctypes.data
+        desc = _lib.SceneDesc()
+        desc.abi_version = _lib.OCTPT_ABI_VERSION
+        desc.octants = ptr(octs)
+        desc.octant_count = t.octant_count
+        desc.root = t.root
+        desc.depth = t.depth
+        desc.leaf_first = ptr(lf)
+        desc.leaf_count = ptr(lc)
+        desc.leaf_table_size = len(lf)
+        desc.leaf_prims = ptr(lp)
+        desc.leaf_prim_count = len(lp)
+        desc.spheres = ptr(self.sphere_structs()) if len(self.spheres) else None
+        desc.sphere_count = len(self.spheres)
+        desc.cuboids = ptr(self.cuboid_structs()) if len(self.cuboids) else None
+        desc.cuboid_count = len(self.cuboids)
+        desc.materials = ptr(mats)
+        desc.material_count = len(self.materials)
+        desc.textures = ptr(texs)
+        desc.texture_count = len(self.textures)
+        desc.sun = self.sun_struct()
+        desc.emitters_enabled = int(self.emitters_enabled)
+        keep.extend([octs, mats, texs])
+        return desc, keep
+
+
+@dataclass
+class RenderSettings:
+    width: int
+    height: int
+    spp: int
+    max_depth: int = 5       # path_tracer.rs:56
+    seed: int = 1
+    branch_count: int = 1    # SURVEY contract C6
+
+
+# ------------------------------------------------------------------------------
+# seeded synthetic scene generator (integer hash -> f32, identical on every machine)
+# ------------------------------------------------------------------------------
+def _lowbias32(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint32)
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x7FEB352D)
+        x ^= x >> np.uint32(15)
+        x *= np.uint32(0x846CA68B)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def scene_uniform(seed: int, stream: int, n: int) -> np.ndarray:
+    """n uniform f32 in [0,1) for (seed, stream): (lowbias32(key ^ i) >> 8) * 2^-24."""
+    key = _lowbias32(np.array([(seed * 0x9E3779B9 + stream * 0x85EBCA6B) & 0xFFFFFFFF], np.uint32))[0]
+    i = np.arange(n, dtype=np.uint32)
+    h = _lowbias32(i ^ key)
+    return (h >> np.uint32(8)).astype(F32) * F32(1.0 / 16777216.0)
+
+
+def _uniform_range(seed, stream, n, lo, hi):
+    u = scene_uniform(seed, stream, n)
+    return F32(lo) + (F32(hi) - F32(lo)) * u
+
+
+DIFFUSE_PALETTE = [(200, 60, 50), (60, 170, 80), (70, 90, 210), (220, 200, 70), (180, 180, 180), (230, 120, 40),
+                   (140, 70, 180), (90, 200, 200)]
+
+
+def primitive_materials(scene: Scene) -> dict:
+    """Standard material set: 8 diffuse colours, metal, glossy, glass (+ air at index 0)."""
+    scene.textures = [Texture()]  # index 0: DEFAULT_TEXTURE for air
+    scene.materials = [air_material(0)]
+    ids = {"diffuse": []}
+    for rgb in DIFFUSE_PALETTE:
+        scene.textures.append(Texture.color(*rgb))
+        scene.materials.append(Material(texture_index=len(scene.textures) - 1))
+        ids["diffuse"].append(len(scene.materials) - 1)
+    scene.textures.append(Texture.color(230, 230, 235))
+    scene.materials.append(Material(metalness=1.0, roughness=0.1, texture_index=len(scene.textures) - 1))
+    ids["metal"] = len(scene.materials) - 1
+    scene.textures.append(Texture.color(240, 240, 240))
+    scene.materials.append(Material(specular=0.3, roughness=0.05, texture_index=len(scene.textures) - 1))
+    ids["glossy"] = len(scene.materials) - 1
+    scene.textures.append(Texture.color(255, 255, 255, 0))
+    scene.materials.append(Material(ior=1.5, flags=REFRACTIVE, texture_index=len(scene.textures) - 1))
+    ids["glass"] = len(scene.materials) - 1
+    return ids
+
+
+def _assign_materials(ids, seed, n, stream=7):
+    """70% diffuse, 15% metal, 10% glossy, 5% glass."""
+    u = scene_uniform(seed, stream, n)
+    pick = scene_uniform(seed, stream + 1, n)
+    mats = np.empty(n, np.uint32)
+    d = np.array(ids["diffuse"], np.uint32)
+    mats[:] = d[np.minimum((pick * len(d)).astype(np.int64), len(d) - 1)]
+    mats[(u >= 0.70) & (u < 0.85)] = ids["metal"]
+    mats[(u >= 0.85) & (u < 0.95)] = ids["glossy"]
+    mats[u >= 0.95] = ids["glass"]
+    return mats
+
+
+def random_spheres(seed: int, n: int, world: float, rmin: float, rmax: float):
+    c = np.stack([_uniform_range(seed, 1 + a, n, 0.0, world) for a in range(3)], axis=1)
+    r = _uniform_range(seed, 4, n, rmin, rmax)
+    return np.concatenate([c, r[:, None]], axis=1).astype(F32)
+
+
+def random_cuboids(seed: int, n: int, world: float, emin: float, emax: float):
+    lo = np.stack([_uniform_range(seed, 11 + a, n, 0.0, world) for a in range(3)], axis=1)
+    ext = np.stack([_uniform_range(seed, 14 + a, n, emin, emax) for a in range(3)], axis=1)
+    return np.concatenate([lo, np.minimum(lo + ext, F32(world - 0.001))], axis=1).astype(F32)
+
+
+CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "tiny")
+
+
+def make_config(name: str, *, seed: int = 1, build: bool = True):
+    """(Scene, Camera, RenderSettings) for BASELINE.json's configs."""
+    sc = Scene()
+    if name in ("C1", "C1-as-is"):
+        ids = primitive_materials(sc)
+        depth = 6
+        sc.spheres = np.array([[32.0, 32.0, 32.0, 4.0]], F32)
+        sc.sphere_material = np.array([ids["diffuse"][0]], np.uint32)
+        cam = Camera(eye=(32.0, 32.0, 8.0), direction=(0.0, 0.0, 1.0), up=(0.0, 1.0, 0.0))
+        rs = RenderSettings(256, 256, 1, max_depth=1, seed=seed)
+        if name == "C1-as-is":  # Scene::hit stubbed to false (scene/mod.rs:172-187): sky + sun only
+            sc.octree = Octree.empty(depth)
+            return sc, cam, rs
+    elif name == "tiny":
+        ids = primitive_materials(sc)
+        depth = 5
+        sc.spheres = random_spheres(seed, 40, 32.0, 0.5, 3.0)
+        sc.sphere_material = _assign_materials(ids, seed, 40)
+        sc.cuboids = random_cuboids(seed, 6, 32.0, 1.0, 4.0)
+        cm = _assign_materials(ids, seed + 5, 6 * 6, stream=21).reshape(6, 6)
+        sc.cuboid_material = cm
+        cam = Camera.look_at((16.0, 20.0, -14.0), (16.0, 16.0, 16.0))
+        rs = RenderSettings(64, 48, 4, seed=seed)
+    elif name == "C2":
+        ids = primitive_materials(sc)
+        depth = 6
+        sc.spheres = random_spheres(seed, 100, 64.0, 0.5, 3.0)
+        sc.sphere_material = _assign_materials(ids, seed, 100)
+        cam = Camera.look_at((32.0, 38.0, -28.0), (32.0, 32.0, 32.0))
+        rs = RenderSettings(1280, 720, 64, seed=seed)
+    elif name == "C3":
+        ids = primitive_materials(sc)
+        depth = 8
+        sc.spheres = random_spheres(seed, 10_000, 256.0, 0.5, 2.5)
+        sc.sphere_material = _assign_materials(ids, seed, 10_000)
+        cam = Camera.look_at((128.0, 150.0, -110.0), (128.0, 128.0, 128.0))
+        rs = RenderSettings(1920, 1080, 256, seed=seed)
+    elif name == "C4":
+        ids = primitive_materials(sc)
+        depth = 10
+        n = 50_000
+        sc.spheres = random_spheres(seed, n, 1024.0, 0.5, 4.0)
+        sc.sphere_material = _assign_materials(ids, seed, n)
+        sc.cuboids = random_cuboids(seed, n, 1024.0, 0.5, 4.0)
+        sc.cuboid_material = _assign_materials(ids, seed + 5, 6 * n, stream=21).reshape(n, 6)
+        cam = Camera.look_at((512.0, 600.0, -420.0), (512.0, 512.0, 512.0))
+        rs = RenderSettings(3840, 2160, 512, seed=seed)
+    else:
+        raise ValueError(f"unknown config {name!r}; known: {CONFIGS}")
+    if build:
+        sc.build_octree(depth)
+    else:
+        sc.octree = None
+        sc._depth = depth  # type: ignore[attr-defined]
+    return sc, cam, rs
+
+
+def load_rgba_fixture(path: str | Path, width: int, height: int) -> np.ndarray:
+    data = np.fromfile(path, dtype=np.uint8)
+    return data.reshape(height, width, 4)

@@ -1,0 +1,20 @@
+"""Diagnostic: C3 render time vs spp (prints after every render)."""
+import sys, time
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+import torch
+from octree_pathtracing_amd import scene as S
+from octree_pathtracing_amd.renderer import HipRenderer
+
+sc, cam, rs = S.make_config(sys.argv[1] if len(sys.argv) > 1 else "C3")
+r = HipRenderer(0)
+r.set_scene(sc); r.set_camera(cam)
+W, H = rs.width, rs.height
+acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"); acc[:, 3] = 1
+for spp in [int(x) for x in (sys.argv[2:] or ["4", "16", "64", "256"])]:
+    r.reset_stats()
+    p = r.params(W, H, 0, spp)
+    torch.cuda.synchronize(); t = time.perf_counter()
+    r.render_device(p, acc.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize(); dt = time.perf_counter() - t
+    st = r.stats()
+    print(f"spp {spp}: {dt*1e3:.1f} ms  {st['segments']/dt/1e6:.1f} Mrays/s  segs/path {st['segments']/st['paths']:.3f} steps/seg {st['esvo_steps']/st['segments']:.1f}", flush=True)
