@@ -132,6 +132,7 @@ typedef struct octpt_camera {
 /* One progressive render call = spp_count passes of TileRenderer::render_tile_average
  * (tile_renderer.rs:684-734) continuing a running mean that already holds spp_start samples. */
 #define OCTPT_RENDER_SHARD_COMPACT 0x1u /* accum holds only this shard's 8x8 tiles, tile-major */
+#define OCTPT_RENDER_MEGAKERNEL 0x2u    /* single persistent megakernel instead of the wavefront loop (A/B) */
 typedef struct octpt_render_params {
     uint32_t width, height;
     uint32_t spp_start, spp_count;
@@ -171,7 +172,9 @@ octpt_status octpt_get_camera(const octpt_ctx *ctx, octpt_camera *camera);
 octpt_status octpt_render(octpt_ctx *ctx, const octpt_render_params *p, float *accum_rgba, uint8_t *out_rgba8);
 
 /* Device-resident render: d_accum is a device pointer (same layout as accum_rgba), the
- * work is enqueued on `hip_stream` (hipStream_t, NULL = default stream) and not waited for.
+ * work is enqueued on `hip_stream` (hipStream_t, NULL = default stream).  The wavefront
+ * loop is steered from the host (it reads back queue lengths), so the call returns once the
+ * last kernel of the render is enqueued, i.e. after the render has essentially finished.
  * d_seg_count (nullable, device, one u32 per accum pixel) receives += ray segments. */
 octpt_status octpt_render_device(octpt_ctx *ctx, const octpt_render_params *p, float *d_accum,
                                  uint32_t *d_seg_count, void *hip_stream);

@@ -27,6 +27,7 @@ ERR_INTERNAL = 7
 TEXTURE_COLOR = 0
 TEXTURE_IMAGE = 1
 RENDER_SHARD_COMPACT = 0x1
+RENDER_MEGAKERNEL = 0x2
 PRIM_NONE = 0xFFFFFFFF
 PRIM_CUBOID_BIT = 0x80000000
 
@@ -160,7 +161,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # OCTPT_LIB: developer override to A/B differently built kernels (same ABI)
+    p = Path(path) if path else Path(os.environ.get("OCTPT_LIB", LIB_PATH))
     try:  # share torch's HIP runtime (same soname libamdhip64.so.7) when torch is present
         import torch  # noqa: F401
     except ImportError:  # pragma: no cover

@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -22,6 +25,16 @@ using namespace octpt;
 namespace {
 
 constexpr uint32_t kCounterRing = 256;
+constexpr uint64_t kMaxChunkPaths = 128ull << 20;  // colour buffer: 2 GiB of float4 per chunk
+constexpr uint32_t kDefaultPool = 4u << 20;          // path slots in flight
+constexpr uint32_t kDefaultRefill = 32;              // extend: idle lanes before a wave refills
+
+uint32_t env_u32(const char *name, uint32_t dflt) {
+    const char *v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    const long x = std::strtol(v, nullptr, 10);
+    return x > 0 ? (uint32_t)x : dflt;
+}
 
 struct EventPair {
     hipEvent_t start, stop;
@@ -58,11 +71,25 @@ struct octpt_ctx {
     double kernel_ms = 0.0;
     uint64_t launches = 0;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
+    int extend_bpc_cache[kMaxDepth + 1] = {0};
+    // wavefront pool (grown on demand)
+    WaveBuffers wb{};
+    size_t pool = 0, color_cap = 0;
+    std::vector<void *> wave_allocs;
+    void *color_alloc = nullptr;
+    uint32_t *h_count = nullptr;  // pinned, 2 entries
+    hipEvent_t count_ev[2] = {nullptr, nullptr};
+    uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
+    // one asynchronous frame may be in flight; device-touching calls join it first
+    octpt_frame *inflight = nullptr;
 };
 
 struct octpt_frame {
     octpt_ctx *ctx = nullptr;
-    hipEvent_t done = nullptr;
+    std::thread worker;
+    std::atomic<bool> finished{false};
+    std::atomic<bool> cancel_requested{false};
+    octpt_status status = OCTPT_OK;
     float *user_accum = nullptr;
     uint8_t *user_rgba = nullptr;
     size_t n_pixels = 0;
@@ -70,7 +97,6 @@ struct octpt_frame {
     uchar4 *d_rgba = nullptr;
     float *h_accum = nullptr;   // pinned
     uint8_t *h_rgba = nullptr;  // pinned
-    bool cancelled = false;
     bool delivered = false;
 };
 
@@ -298,29 +324,133 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
 
 size_t accum_pixels(const DevRender &R) { return R.compact ? (size_t)R.total_items : (size_t)R.W * R.H; }
 
-octpt_status enqueue_render(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s) {
-    if (R.spp_count == 0 || R.total_items == 0) return OCTPT_OK;
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
+void free_wave(octpt_ctx *ctx) {
+    for (void *p : ctx->wave_allocs) (void)hipFree(p);
+    ctx->wave_allocs.clear();
+    if (ctx->color_alloc) (void)hipFree(ctx->color_alloc);
+    ctx->color_alloc = nullptr;
+    ctx->pool = ctx->color_cap = 0;
+    ctx->wb = WaveBuffers{};
+}
+
+template <class T>
+hipError_t wave_alloc(octpt_ctx *ctx, size_t n, T **out) {
+    void *p = nullptr;
+    const hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess) return e;
+    ctx->wave_allocs.push_back(p);
+    *out = static_cast<T *>(p);
+    return hipSuccess;
+}
+
+octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
+    if (!ctx->h_count) {
+        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), 2 * sizeof(uint32_t), hipHostMallocDefault));
+        for (auto &ev : ctx->count_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    if (pool > ctx->pool) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        for (void *p : ctx->wave_allocs) (void)hipFree(p);
+        ctx->wave_allocs.clear();
+        ctx->pool = 0;
+        WaveBuffers &B = ctx->wb;
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray0[0]));
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray0[1]));
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray1[0]));
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray1[1]));
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pa));
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pb));
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pc));
+        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.hit));
+        HIP_TRY(ctx, wave_alloc(ctx, 1, &B.ctrl));
+        ctx->pool = pool;
+    }
+    if (color_items > ctx->color_cap) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (ctx->color_alloc) (void)hipFree(ctx->color_alloc);
+        ctx->color_alloc = nullptr;
+        ctx->color_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&ctx->color_alloc, color_items * sizeof(float4)));
+        ctx->color_cap = color_items;
+    }
+    ctx->wb.color = static_cast<float4 *>(ctx->color_alloc);
+    return OCTPT_OK;
+}
+
+// megakernel variant (OCTPT_RENDER_MEGAKERNEL): one persistent launch per call
+octpt_status enqueue_megakernel(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s) {
     uint32_t *counter = ctx->d_counters + (ctx->launch_seq++ % kCounterRing);
     HIP_TRY(ctx, hipMemsetAsync(counter, 0, sizeof(uint32_t), s));
     int &bpc = ctx->blocks_per_cu_cache[ctx->S.depth];
     if (bpc == 0) bpc = render_blocks_per_cu(ctx->S.depth);
     const uint64_t needed = ((uint64_t)R.total_items + kBlock - 1) / kBlock;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(needed, (uint64_t)ctx->num_cu * bpc));
+    HIP_TRY(ctx, launch_render(ctx->S, ctx->C, R, d_accum, d_seg, counter, ctx->d_stats, grid, s));
+    return OCTPT_OK;
+}
+
+// wavefront path tracer: per chunk of passes, seed the path pool, then
+// alternate extend/shade until the ray queue drains, then resolve the running means.  The
+// host steers the loop with a one-iteration lookahead on the queue length.
+octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s,
+                               const std::atomic<bool> *cancel) {
+    const uint64_t n_px = R.total_items;
+    const uint32_t chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, kMaxChunkPaths / n_px));
+    const uint64_t chunk_max = (uint64_t)chunk_spp * n_px;
+    const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
+    octpt_status st = ensure_wave(ctx, pool, chunk_max);
+    if (st != OCTPT_OK) return st;
+    int &bpc = ctx->extend_bpc_cache[ctx->S.depth];
+    if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S.depth);
+    const int grid_extend = ctx->num_cu * bpc;
+    const int grid_shade = ctx->num_cu * 4;
+    const WaveBuffers &B = ctx->wb;
+    for (uint32_t c0 = 0; c0 < R.spp_count; c0 += chunk_spp) {
+        DevRender Rc = R;
+        Rc.spp_start = R.spp_start + c0;
+        Rc.spp_count = std::min(chunk_spp, R.spp_count - c0);
+        const uint32_t chunk_items = (uint32_t)((uint64_t)Rc.spp_count * n_px);
+        HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, sizeof(WaveCtrl), s));
+        const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
+        HIP_TRY(ctx, launch_wf_seed(ctx->C, Rc, B, n_seed, chunk_items, ctx->d_stats, s));
+        for (uint32_t it = 0;; ++it) {
+            if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
+            const uint32_t q = it & 1u;
+            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, grid_extend, ctx->d_stats, s));
+            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, grid_shade, ctx->d_stats, s));
+            HIP_TRY(ctx, hipMemcpyAsync(&ctx->h_count[q], &B.ctrl->count[q ^ 1u], sizeof(uint32_t),
+                                        hipMemcpyDeviceToHost, s));
+            HIP_TRY(ctx, hipEventRecord(ctx->count_ev[q], s));
+            if (it >= 1) {
+                HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[q ^ 1u]));
+                if (ctx->h_count[q ^ 1u] == 0u) break;  // iteration `it` had nothing to do
+            }
+        }
+        HIP_TRY(ctx, launch_wf_resolve(Rc, B, Rc.spp_count, d_accum, d_seg, s));
+    }
+    return OCTPT_OK;
+}
+
+octpt_status enqueue_render(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s,
+                            bool megakernel, const std::atomic<bool> *cancel = nullptr) {
+    if (R.spp_count == 0 || R.total_items == 0) return OCTPT_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
     EventPair ev{};
     HIP_TRY(ctx, hipEventCreate(&ev.start));
     HIP_TRY(ctx, hipEventCreate(&ev.stop));
+    ctx->pending.push_back(ev);  // destroyed by get_stats / destroy
     HIP_TRY(ctx, hipEventRecord(ev.start, s));
-    hipError_t e = launch_render(ctx->S, ctx->C, R, d_accum, d_seg, counter, ctx->d_stats, grid, s);
-    if (e != hipSuccess) {
-        (void)hipEventDestroy(ev.start);
-        (void)hipEventDestroy(ev.stop);
-        return hip_fail(ctx, e, "render_kernel launch");
-    }
+    octpt_status st = megakernel ? enqueue_megakernel(ctx, R, d_accum, d_seg, s)
+                                 : enqueue_wavefront(ctx, R, d_accum, d_seg, s, cancel);
     HIP_TRY(ctx, hipEventRecord(ev.stop, s));
-    ctx->pending.push_back(ev);
-    ctx->launches++;
-    return OCTPT_OK;
+    if (st == OCTPT_OK) ctx->launches++;
+    return st;
+}
+
+void join_inflight(octpt_ctx *ctx) {
+    octpt_frame *f = ctx->inflight;
+    if (f && f->worker.joinable()) f->worker.join();
+    ctx->inflight = nullptr;
 }
 
 void free_frame_buffers(octpt_frame *f) {
@@ -328,16 +458,14 @@ void free_frame_buffers(octpt_frame *f) {
     if (f->d_rgba) (void)hipFree(f->d_rgba);
     if (f->h_accum) (void)hipHostFree(f->h_accum);
     if (f->h_rgba) (void)hipHostFree(f->h_rgba);
-    if (f->done) (void)hipEventDestroy(f->done);
     f->d_accum = nullptr;
     f->d_rgba = nullptr;
     f->h_accum = nullptr;
     f->h_rgba = nullptr;
-    f->done = nullptr;
 }
 
 void deliver(octpt_frame *f) {
-    if (f->delivered || f->cancelled) return;
+    if (f->delivered) return;
     std::memcpy(f->user_accum, f->h_accum, f->n_pixels * 16);
     if (f->user_rgba) std::memcpy(f->user_rgba, f->h_rgba, f->n_pixels * 4);
     f->delivered = true;
@@ -423,6 +551,8 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return bail(OCTPT_ERR_DEVICE);
     ctx->device = device;
     ctx->num_cu = prop.multiProcessorCount;
+    ctx->pool_cap = env_u32("OCTPT_POOL", kDefaultPool);
+    ctx->refill = std::min<uint32_t>(env_u32("OCTPT_REFILL", kDefaultRefill), 64u);
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);
@@ -441,6 +571,7 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
 
 void octpt_destroy(octpt_ctx *ctx) {
     if (!ctx) return;
+    join_inflight(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto &e : ctx->pending) {
@@ -449,6 +580,10 @@ void octpt_destroy(octpt_ctx *ctx) {
         (void)hipEventDestroy(e.stop);
     }
     free_scene(ctx);
+    free_wave(ctx);
+    if (ctx->h_count) (void)hipHostFree(ctx->h_count);
+    for (auto &ev : ctx->count_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_lut_float) (void)hipFree(ctx->d_lut_float);
@@ -461,6 +596,7 @@ const char *octpt_last_error(const octpt_ctx *ctx) { return ctx ? ctx->err.c_str
 
 octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    join_inflight(ctx);
     try {
         octpt_status st = validate_scene(ctx, d);
         if (st != OCTPT_OK) return st;
@@ -468,13 +604,23 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         free_scene(ctx);
         DevScene S{};
-        std::vector<uint32_t> mask(d->octant_count), children((size_t)d->octant_count * 8);
+        // packed child slots: one 8-byte load per descend / leaf visit
+        std::vector<uint2> child((size_t)d->octant_count * 8, make_uint2(0u, 0u));
         for (uint32_t n = 0; n < d->octant_count; ++n) {
-            mask[n] = d->octants[n].child_mask;
-            std::memcpy(&children[(size_t)n * 8], d->octants[n].children, 32);
+            const octpt_octant &o = d->octants[n];
+            for (int i = 0; i < 8; ++i) {
+                const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+                if (!present) continue;
+                const uint32_t v = o.children[i];
+                if (!leaf) {
+                    child[(size_t)n * 8 + i] = make_uint2(v, d->octants[v].child_mask);
+                } else if (d->leaf_count[v] == 1) {  // single-primitive leaf: the prim id itself
+                    child[(size_t)n * 8 + i] = make_uint2(d->leaf_prims[d->leaf_first[v]], 1u);
+                } else {
+                    child[(size_t)n * 8 + i] = make_uint2(d->leaf_first[v], d->leaf_count[v]);
+                }
+            }
         }
-        std::vector<uint2> ranges(d->leaf_table_size);
-        for (uint32_t l = 0; l < d->leaf_table_size; ++l) ranges[l] = make_uint2(d->leaf_first[l], d->leaf_count[l]);
         std::vector<float4> sph(d->sphere_count);
         std::vector<uint32_t> sph_mat(d->sphere_count);
         for (uint32_t s = 0; s < d->sphere_count; ++s) {
@@ -490,10 +636,29 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
             cmax[c] = make_float4(x.max[0], x.max[1], x.max[2], 0.0f);
             std::memcpy(&cmat[(size_t)c * 6], x.face_material, 24);
         }
+        float lf[256];
+        uint8_t lb[256];
+        make_luts(lf, lb);
         std::vector<DevMaterial> mats(d->material_count);
         for (uint32_t m = 0; m < d->material_count; ++m) {
             const octpt_material &x = d->materials[m];
-            mats[m] = DevMaterial{x.ior, x.specular, x.emittance, x.roughness, x.metalness, x.texture_index, x.tint_index, x.flags};
+            const octpt_texture &t = d->textures[x.texture_index];
+            DevMaterial dm{};
+            dm.ior = x.ior;
+            dm.specular = x.specular;
+            dm.emittance = x.emittance;
+            dm.roughness = x.roughness;
+            dm.metalness = x.metalness;
+            dm.texture_index = x.texture_index;
+            dm.flags = x.flags;
+            dm.texture_kind = t.kind;
+            if (t.kind == OCTPT_TEXTURE_COLOR) {  // F32Color::from(&U8Color) (colors/mod.rs:280-288)
+                dm.color[0] = lf[t.rgba[0]];
+                dm.color[1] = lf[t.rgba[1]];
+                dm.color[2] = lf[t.rgba[2]];
+                dm.color[3] = (float)t.rgba[3] / 255.0f;
+            }
+            mats[m] = dm;
         }
         std::vector<DevTexture> texs(d->texture_count);
         std::vector<uint8_t> texels;
@@ -510,15 +675,13 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
             }
             texs[t] = dt;
         }
-        uint32_t *d_mask, *d_children, *d_prims, *d_sph_mat, *d_cmat;
-        uint2 *d_ranges;
+        uint32_t *d_prims, *d_sph_mat, *d_cmat;
+        uint2 *d_child;
         float4 *d_sph, *d_cmin, *d_cmax;
         DevMaterial *d_mats;
         DevTexture *d_texs;
         uint8_t *d_texels;
-        HIP_TRY(ctx, upload(ctx, mask.data(), mask.size(), &d_mask));
-        HIP_TRY(ctx, upload(ctx, children.data(), children.size(), &d_children));
-        HIP_TRY(ctx, upload(ctx, ranges.data(), ranges.size(), &d_ranges));
+        HIP_TRY(ctx, upload(ctx, child.data(), child.size(), &d_child));
         HIP_TRY(ctx, upload(ctx, d->leaf_prims, d->leaf_prim_count, &d_prims));
         HIP_TRY(ctx, upload(ctx, sph.data(), sph.size(), &d_sph));
         HIP_TRY(ctx, upload(ctx, sph_mat.data(), sph_mat.size(), &d_sph_mat));
@@ -528,13 +691,15 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         HIP_TRY(ctx, upload(ctx, mats.data(), mats.size(), &d_mats));
         HIP_TRY(ctx, upload(ctx, texs.data(), texs.size(), &d_texs));
         HIP_TRY(ctx, upload(ctx, texels.data(), texels.size(), &d_texels));
-        S.node_mask = d_mask;
-        S.node_children = d_children;
+        S.node_child = d_child;
         S.root = d->root;
+        S.root_mask = d->octants[d->root].child_mask;
+        S.node0_mask = d->octants[0].child_mask;
         S.depth = d->depth;
         S.n_octants = d->octant_count;
+        S.has_cuboids = d->cuboid_count ? 1u : 0u;
         S.octree_scale = ldexpf(1.0f, -(int)d->depth);  // Octree::scale (new_octree.rs:40-42)
-        S.leaf_range = d_ranges;
+        S.inv_octree_scale = ldexpf(1.0f, (int)d->depth);
         S.leaf_prims = d_prims;
         S.spheres = d_sph;
         S.sphere_mat = d_sph_mat;
@@ -545,9 +710,6 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.texs = d_texs;
         S.texels = d_texels;
         S.lut_float = ctx->d_lut_float;
-        float lf[256];
-        uint8_t lb[256];
-        make_luts(lf, lb);
         make_sun(d->sun, lf, S.sun);
         S.emitters = d->emitters_enabled ? 1 : 0;
         ctx->S = S;
@@ -591,14 +753,54 @@ octpt_status octpt_render_device(octpt_ctx *ctx, const octpt_render_params *p, f
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
     if (!d_accum) return fail(ctx, OCTPT_ERR_INVALID_ARG, "d_accum NULL");
     try {
+        join_inflight(ctx);
         DevRender R{};
         octpt_status st = make_render(ctx, p, R);
         if (st != OCTPT_OK) return st;
-        return enqueue_render(ctx, R, reinterpret_cast<float4 *>(d_accum), d_seg, static_cast<hipStream_t>(stream));
+        return enqueue_render(ctx, R, reinterpret_cast<float4 *>(d_accum), d_seg, static_cast<hipStream_t>(stream),
+                              (p->flags & OCTPT_RENDER_MEGAKERNEL) != 0);
     } catch (...) {
         return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in render");
     }
 }
+
+namespace {
+// FrameInFlight worker: H2D, render, tone map, D2H on the context stream
+void frame_worker(octpt_frame *f, DevRender R, bool megakernel) {
+    octpt_ctx *ctx = f->ctx;
+    octpt_status st = OCTPT_OK;
+    auto run = [&]() -> octpt_status {
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        HIP_TRY(ctx, hipMemcpyAsync(f->d_accum, f->h_accum, f->n_pixels * 16, hipMemcpyHostToDevice, ctx->stream));
+        octpt_status r = enqueue_render(ctx, R, f->d_accum, nullptr, ctx->stream, megakernel, &f->cancel_requested);
+        if (r != OCTPT_OK) return r;
+        if (f->d_rgba) {
+            HIP_TRY(ctx, launch_tonemap(f->d_accum, f->d_rgba, (uint32_t)f->n_pixels, ctx->d_lut_byte, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(f->h_rgba, f->d_rgba, f->n_pixels * 4, hipMemcpyDeviceToHost, ctx->stream));
+        }
+        HIP_TRY(ctx, hipMemcpyAsync(f->h_accum, f->d_accum, f->n_pixels * 16, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OCTPT_OK;
+    };
+    try {
+        st = run();
+    } catch (...) {
+        st = fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in frame worker");
+    }
+    if (st != OCTPT_OK) (void)hipStreamSynchronize(ctx->stream);
+    f->status = st;
+    f->finished.store(true);
+}
+
+octpt_status frame_result(octpt_frame *f) {
+    if (f->worker.joinable()) f->worker.join();
+    if (f->ctx && f->ctx->inflight == f) f->ctx->inflight = nullptr;
+    if (f->cancel_requested.load()) return OCTPT_CANCELLED;
+    if (f->status != OCTPT_OK) return f->status;
+    deliver(f);
+    return OCTPT_OK;
+}
+}  // namespace
 
 octpt_status octpt_render_async(octpt_ctx *ctx, const octpt_render_params *p, float *accum, uint8_t *rgba,
                                 octpt_frame **out) {
@@ -607,6 +809,7 @@ octpt_status octpt_render_async(octpt_ctx *ctx, const octpt_render_params *p, fl
     *out = nullptr;
     octpt_frame *f = nullptr;
     try {
+        join_inflight(ctx);
         DevRender R{};
         octpt_status st = make_render(ctx, p, R);
         if (st != OCTPT_OK) return st;
@@ -630,30 +833,14 @@ octpt_status octpt_render_async(octpt_ctx *ctx, const octpt_render_params *p, fl
             if ((e = hipHostMalloc(&f->h_rgba, f->n_pixels * 4, hipHostMallocDefault)) != hipSuccess)
                 return fail_frame(e, "hipHostMalloc rgba");
         }
-        if ((e = hipEventCreateWithFlags(&f->done, hipEventDisableTiming)) != hipSuccess) return fail_frame(e, "event");
         std::memcpy(f->h_accum, accum, f->n_pixels * 16);
-        if ((e = hipMemcpyAsync(f->d_accum, f->h_accum, f->n_pixels * 16, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
-            return fail_frame(e, "H2D accum");
-        st = enqueue_render(ctx, R, f->d_accum, nullptr, ctx->stream);
-        if (st != OCTPT_OK) {
-            (void)hipStreamSynchronize(ctx->stream);
-            free_frame_buffers(f);
-            delete f;
-            return st;
-        }
-        if (rgba) {
-            if ((e = launch_tonemap(f->d_accum, f->d_rgba, (uint32_t)f->n_pixels, ctx->d_lut_byte, ctx->stream)) != hipSuccess)
-                return fail_frame(e, "tonemap launch");
-            if ((e = hipMemcpyAsync(f->h_rgba, f->d_rgba, f->n_pixels * 4, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
-                return fail_frame(e, "D2H rgba");
-        }
-        if ((e = hipMemcpyAsync(f->h_accum, f->d_accum, f->n_pixels * 16, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
-            return fail_frame(e, "D2H accum");
-        if ((e = hipEventRecord(f->done, ctx->stream)) != hipSuccess) return fail_frame(e, "event record");
+        f->worker = std::thread(frame_worker, f, R, (p->flags & OCTPT_RENDER_MEGAKERNEL) != 0);
+        ctx->inflight = f;
         *out = f;
         return OCTPT_OK;
     } catch (...) {
         if (f) {
+            if (f->worker.joinable()) f->worker.join();
             free_frame_buffers(f);
             delete f;
         }
@@ -663,35 +850,25 @@ octpt_status octpt_render_async(octpt_ctx *ctx, const octpt_render_params *p, fl
 
 octpt_status octpt_frame_poll(octpt_frame *f) {
     if (!f) return OCTPT_ERR_INVALID_ARG;
-    if (f->cancelled) return OCTPT_CANCELLED;
-    if (f->delivered) return OCTPT_OK;
-    const hipError_t e = hipEventQuery(f->done);
-    if (e == hipErrorNotReady) return OCTPT_NOT_READY;
-    if (e != hipSuccess) return hip_fail(f->ctx, e, "frame poll");
-    deliver(f);
-    return OCTPT_OK;
+    if (!f->finished.load()) return OCTPT_NOT_READY;
+    return frame_result(f);
 }
 
 octpt_status octpt_frame_wait(octpt_frame *f) {
     if (!f) return OCTPT_ERR_INVALID_ARG;
-    if (f->cancelled) return OCTPT_CANCELLED;
-    if (!f->delivered) {
-        const hipError_t e = hipEventSynchronize(f->done);
-        if (e != hipSuccess) return hip_fail(f->ctx, e, "frame wait");
-        deliver(f);
-    }
-    return OCTPT_OK;
+    return frame_result(f);
 }
 
 octpt_status octpt_frame_cancel(octpt_frame *f) {
     if (!f) return OCTPT_ERR_INVALID_ARG;
-    if (!f->delivered) f->cancelled = true;
+    if (!f->delivered) f->cancel_requested.store(true);
     return OCTPT_OK;
 }
 
 void octpt_frame_release(octpt_frame *f) {
     if (!f) return;
-    if (f->done) (void)hipEventSynchronize(f->done);  // buffers may still be in use by the stream
+    if (f->worker.joinable()) f->worker.join();
+    if (f->ctx && f->ctx->inflight == f) f->ctx->inflight = nullptr;
     free_frame_buffers(f);
     delete f;
 }
@@ -735,6 +912,7 @@ octpt_status octpt_unshard_device(octpt_ctx *ctx, uint32_t W, uint32_t H, uint32
 octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *last_prim, const float *last_normal,
                              uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps) {
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    join_inflight(ctx);
     if (!ctx->has_scene) return fail(ctx, OCTPT_ERR_INVALID_ARG, "no scene uploaded");
     if (n == 0) return OCTPT_OK;
     if (!rays || !t || !prim) return fail(ctx, OCTPT_ERR_INVALID_ARG, "NULL buffer");
@@ -776,6 +954,7 @@ octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *
 octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     if (!cctx || !out) return OCTPT_ERR_INVALID_ARG;
     octpt_ctx *ctx = const_cast<octpt_ctx *>(cctx);
+    join_inflight(ctx);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     for (auto &e : ctx->pending) {
         HIP_TRY(ctx, hipEventSynchronize(e.stop));
@@ -802,6 +981,7 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
 
 octpt_status octpt_reset_stats(octpt_ctx *ctx) {
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    join_inflight(ctx);
     octpt_stats tmp;
     octpt_status st = octpt_get_stats(ctx, &tmp);  // drains pending events
     if (st != OCTPT_OK) return st;

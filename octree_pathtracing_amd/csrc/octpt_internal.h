@@ -12,11 +12,13 @@ constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primar
 constexpr uint32_t kBlock = 256;       // threads per block (4 waves)
 constexpr uint32_t kMaxDepth = 21;     // new_octree.rs:14
 
-// GPUMaterial (gpu_material.rs:67-76), 32 B: fetched as two float4
+// GPUMaterial (gpu_material.rs:67-76) + the material's texture kind and, for colour
+// textures, the pre-converted F32Color (colors/mod.rs:280-288): 48 B, three float4 loads
 struct alignas(16) DevMaterial {
     float ior, specular, emittance, roughness;
     float metalness;
-    uint32_t texture_index, tint_index, flags;
+    uint32_t texture_index, flags, texture_kind;
+    float color[4];
 };
 
 // texture table entry, 16 B
@@ -44,11 +46,13 @@ struct DevSun {
 };
 
 struct DevScene {
-    const uint32_t *node_mask;      // per octant: child_mask (bit i present, bit i+8 leaf)
-    const uint32_t *node_children;  // 8 per octant
-    uint32_t root, depth, n_octants;
+    // 8 packed child slots per octant: octant child = (index, its child_mask),
+    // leaf child = (first leaf prim, prim count), empty = (0, 0)
+    const uint2 *node_child;
+    uint32_t root, root_mask, node0_mask, depth, n_octants;
+    uint32_t has_cuboids;
     float octree_scale;             // 2^-depth
-    const uint2 *leaf_range;        // (first, count) per leaf payload
+    float inv_octree_scale;         // 2^depth (x / 2^-depth == x * 2^depth exactly)
     const uint32_t *leaf_prims;
     const float4 *spheres;          // (cx, cy, cz, r)
     const uint32_t *sphere_mat;
@@ -81,6 +85,25 @@ struct DevRender {
     float dim;               // max(W, H)
 };
 
+// wavefront path tracer state
+struct WaveCtrl {
+    uint32_t count[2];   // rays queued in queue[q]
+    uint32_t head[2];    // extend's read cursor into queue[q]
+    uint32_t next_item;  // next chunk work item (pixel x sample) to start
+    uint32_t pad[3];
+};
+
+struct WaveBuffers {
+    float4 *ray0[2];  // per queue position: (o.xyz, last_prim)
+    float4 *ray1[2];  // per queue position: (d.xyz, slot | self_inward << 31)
+    float4 *pa;     // (T.xyz, L.x)
+    float4 *pb;     // (L.y, L.z, rng, item)
+    uint2 *pc;      // (cur_mat, depth | specular << 8 | path_segs << 16)
+    uint4 *hit;     // per queue position: (prim, t, inside | axis << 1 | neg << 3, -)
+    float4 *color;  // per chunk item: (L.xyz, path segments)
+    WaveCtrl *ctrl;
+};
+
 // per-launch statistics, accumulated with one atomic per wave
 enum StatIndex {
     kStatPaths = 0,
@@ -97,6 +120,15 @@ enum StatIndex {
 hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
                          uint32_t *segcount, uint32_t *counter, unsigned long long *stats, int grid,
                          hipStream_t stream);
+hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t n_seed,
+                          uint32_t chunk_items, unsigned long long *stats, hipStream_t stream);
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
+                            unsigned long long *stats, hipStream_t stream);
+hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
+                           uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream);
+hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,
+                             uint32_t *segcount, hipStream_t stream);
+int extend_blocks_per_cu(uint32_t depth);
 hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t *last_prim,
                             const float *last_normal, uint32_t n, float *t, uint32_t *prim, float *normal,
                             uint32_t *steps, hipStream_t stream);

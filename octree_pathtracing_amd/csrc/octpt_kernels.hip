@@ -161,19 +161,35 @@ __device__ __forceinline__ float rng_next(uint32_t &st) {
 }
 
 // ---------------------------------------------------------------------------
-// ray / path state
+// rays, path state, counters
 // ---------------------------------------------------------------------------
-struct PathRay {
+// What a closest-hit query needs (Scene::hit): origin, direction and the self-intersection
+// key of contract C2 (last primitive + whether the ray points into it).
+struct TraceRay {
+    v3 o, d;
+    uint32_t last_prim;
+    bool self_inward;
+};
+
+// ESVO stack in LDS: (octant, t_max) + the octant's child mask, [slot][thread] rows
+struct Stack {
+    uint2 *e;
+    uint16_t *m;
+};
+
+// Path state between segments (Ray + HitRecord of ray/mod.rs:16-23, hittable/mod.rs:53-84,
+// plus the forward throughput T / radiance L of the kernel's accumulation order).
+struct PathState {
     v3 o, d, n;
     float col[4];
-    float u, v, t;
-    uint32_t cur, prev, depth, last_prim;
+    v3 T, L;
+    uint32_t cur, prev, depth, last_prim, path_segs, rng;
     bool specular;
 };
 
 struct Esvo {
     v3 t_coef, t_bias, pos;
-    float t_min, t_max, h, scale_exp2, max_dst;
+    float t_min, t_max, h, scale_exp2;
     uint32_t parent, pmask, idx, mirror, scale, iter;
 };
 
@@ -187,17 +203,11 @@ __device__ __forceinline__ uint32_t f2u32_sat(float f) {
     return (uint32_t)f;
 }
 
-// Texture::value (texture.rs:64-93), corrected RGBA stride [C9]
-__device__ inline void texture_value(const DevScene &S, uint32_t tex_idx, float u, float v, float out[4],
-                                     Counters &cnt) {
+// Texture::value (texture.rs:64-93) for Texture::Image, corrected RGBA stride [C9]; colour
+// textures are pre-converted into the material record at upload
+__device__ inline void texture_image_value(const DevScene &S, uint32_t tex_idx, float u, float v, float out[4],
+                                           Counters &cnt) {
     const DevTexture t = S.texs[tex_idx];
-    if (t.kind == 0u) {  // F32Color::from(&U8Color) (colors/mod.rs:280-288)
-        out[0] = S.lut_float[t.rgba & 255u];
-        out[1] = S.lut_float[(t.rgba >> 8) & 255u];
-        out[2] = S.lut_float[(t.rgba >> 16) & 255u];
-        out[3] = (float)(t.rgba >> 24) / 255.0f;
-        return;
-    }
     if (t.height == 0u) { out[0] = out[1] = out[2] = out[3] = 1.0f; return; }
     float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
     float vv = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
@@ -222,7 +232,7 @@ struct PrimHit {
 };
 
 // Sphere::hit restated (sphere.rs:33-57) + root selection [C2]
-__device__ __forceinline__ bool sphere_test(float4 sp, const PathRay &r, bool self_prim, PrimHit &h) {
+__device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool self_prim, PrimHit &h) {
     const v3 oc = vsub(V(sp.x, sp.y, sp.z), r.o);
     const float a = vdot(r.d, r.d);
     const float hh = vdot(r.d, oc);
@@ -233,7 +243,7 @@ __device__ __forceinline__ bool sphere_test(float4 sp, const PathRay &r, bool se
     const float t0 = (hh - sq) / a;
     const float t1 = (hh + sq) / a;
     if (self_prim) {
-        if (vdot(r.d, r.n) < 0.0f && t1 > RAY_EPSILON) { h.t = t1; h.inside = 1u; return true; }
+        if (r.self_inward && t1 > RAY_EPSILON) { h.t = t1; h.inside = 1u; return true; }
         return false;
     }
     if (t0 > RAY_EPSILON) { h.t = t0; h.inside = 0u; return true; }
@@ -244,7 +254,8 @@ __device__ __forceinline__ bool sphere_test(float4 sp, const PathRay &r, bool se
 __device__ __forceinline__ float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6f : 1.0f / d; }
 
 // AABB::intersects_new (aabb.rs:172-191) [C3]
-__device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const PathRay &r, bool self_prim, PrimHit &h) {
+__device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const TraceRay &r, bool self_prim, PrimHit &h) {
+    // Ray::set_direction's clamped 1/d (mod.rs:91-112), derived from the direction [C12]
     const v3 inv = V(inv_clamped(r.d.x), inv_clamped(r.d.y), inv_clamped(r.d.z));
     const v3 tb = vmul(vsub(V(bmin.x, bmin.y, bmin.z), r.o), inv);
     const v3 tt = vmul(vsub(V(bmax.x, bmax.y, bmax.z), r.o), inv);
@@ -257,7 +268,7 @@ __device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const Path
     uint32_t inside;
     float t;
     if (self_prim) {
-        if (!(vdot(r.d, r.n) < 0.0f && t1 > RAY_EPSILON)) return false;
+        if (!(r.self_inward && t1 > RAY_EPSILON)) return false;
         inside = 1u; t = t1;
     } else if (t0 > RAY_EPSILON) {
         inside = 0u; t = t0;
@@ -284,7 +295,7 @@ __device__ __forceinline__ uint32_t face_index(uint32_t axis, float sgn) {
 }
 
 // Chunky-style commit [C1]: the ray origin moves to the hit point
-__device__ inline void commit_hit(const DevScene &S, PathRay &r, uint32_t prim, const PrimHit &h, Counters &cnt) {
+__device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim, const PrimHit &h, Counters &cnt) {
     const v3 p = vadd(r.o, vscale(r.d, h.t));
     float u = 0.0f, v = 0.0f;
     uint32_t mat;
@@ -317,7 +328,6 @@ __device__ inline void commit_hit(const DevScene &S, PathRay &r, uint32_t prim, 
         uv_ready = true;
     }
     r.o = p;
-    r.t = h.t;
     r.n = n;
     r.last_prim = prim;
     if (h.inside) {
@@ -325,35 +335,59 @@ __device__ inline void commit_hit(const DevScene &S, PathRay &r, uint32_t prim, 
         r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;
     } else {
         r.cur = mat;
-        const uint32_t tex = S.mats[mat].texture_index;
-        if (!uv_ready && S.texs[tex].kind != 0u) {
-            const float theta = dm_acos(-n.y);  // Sphere::get_uv (sphere.rs:60-69)
-            const float phi = dm_atan2(-n.z, n.x) + PI_F;
-            u = phi / (2.0f * PI_F);
-            v = theta / PI_F;
+        const DevMaterial &m = S.mats[mat];
+        if (m.texture_kind == 0u) {
+            r.col[0] = m.color[0];
+            r.col[1] = m.color[1];
+            r.col[2] = m.color[2];
+            r.col[3] = m.color[3];
+        } else {
+            if (!uv_ready) {
+                const float theta = dm_acos(-n.y);  // Sphere::get_uv (sphere.rs:60-69)
+                const float phi = dm_atan2(-n.z, n.x) + PI_F;
+                u = phi / (2.0f * PI_F);
+                v = theta / PI_F;
+            }
+            texture_image_value(S, m.texture_index, u, v, r.col, cnt);
         }
-        texture_value(S, tex, u, v, r.col, cnt);
     }
-    r.u = u;
-    r.v = v;
 }
 
 // ---------------------------------------------------------------------------
 // ESVO (octree_traversal.rs:54-302) split into setup + one iteration
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void stk_write(uint2 *stk, uint32_t slot, uint32_t node, float t) {
-    stk[slot * kBlock] = make_uint2(node, __float_as_uint(t));
+__device__ __forceinline__ void stk_write(const Stack &stk, uint32_t slot, uint32_t node, float t, uint32_t mask) {
+    stk.e[slot * kBlock] = make_uint2(node, __float_as_uint(t));
+    stk.m[slot * kBlock] = (uint16_t)mask;
 }
 
-__device__ inline void esvo_begin(const DevScene &S, const PathRay &ray, Esvo &E, uint2 *stk) {
+__device__ __forceinline__ Stack stack_of(uint2 *lds, uint32_t depth) {
+    Stack s;
+    s.e = lds + threadIdx.x;
+    s.m = reinterpret_cast<uint16_t *>(lds + (size_t)depth * kBlock) + threadIdx.x;
+    return s;
+}
+
+__device__ __forceinline__ TraceRay make_trace_ray(const DevScene &S, v3 o, v3 d, uint32_t last_prim, bool inward) {
+    TraceRay t;
+    t.o = o;
+    t.d = d;
+    t.last_prim = last_prim;
+    t.self_inward = inward;
+    return t;
+}
+
+__device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const Stack &stk) {
     const float osc = S.octree_scale;
-    for (uint32_t s = 0; s < S.depth; ++s) stk_write(stk, s, 0u, 0.0f);
+    // The reference zero-initialises the stack (octree_traversal.rs:69-70).  ESVO only pops to a
+    // scale it pushed during the same ray (a push is skipped only when the entry already holds the
+    // same parent), so stale entries are never read and the zeroing is omitted; the oracle keeps it
+    // and the parity tests would expose any violation.
     v3 ro = vscale(ray.o, osc);
     v3 rd = ray.d;
-    E.max_dst = MAX_DST_WORLD * osc;
     ro = vadd(ro, V(1.0f, 1.0f, 1.0f));
     E.parent = S.root;
-    E.pmask = S.node_mask[S.root];
+    E.pmask = S.root_mask;
     E.scale = OCTREE_MAX_SCALE - 1u;
     E.scale_exp2 = 0.5f;
     const uint32_t epsb = __float_as_uint(OCTREE_EPSILON) & 0x7FFFFFFFu;
@@ -380,14 +414,14 @@ __device__ inline void esvo_begin(const DevScene &S, const PathRay &ray, Esvo &E
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 
-// leaf primitive list test [C1]
-__device__ inline bool leaf_test(const DevScene &S, const PathRay &r, uint32_t leaf, float t_exit_w, float cell_w,
+// leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
+// common single-primitive leaf (one dependent load fewer).
+__device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_exit_w, float cell_w,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt) {
-    const uint2 lr = S.leaf_range[leaf];
     const float t_accept = t_exit_w + CELL_TOL * cell_w;
     bool found = false;
     for (uint32_t k = 0; k < lr.y; ++k) {
-        const uint32_t prim = S.leaf_prims[lr.x + k];
+        const uint32_t prim = lr.y == 1u ? lr.x : S.leaf_prims[lr.x + k];
         const bool self_prim = prim == r.last_prim;
         PrimHit h;
         bool ok;
@@ -408,9 +442,12 @@ __device__ inline bool leaf_test(const DevScene &S, const PathRay &r, uint32_t l
     return found;
 }
 
-__device__ inline int esvo_step(const DevScene &S, PathRay &ray, Esvo &E, uint2 *stk, Counters &cnt) {
+// one ESVO iteration; on kStepHit (prim, h) hold the accepted primitive hit
+__device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const Stack &stk, Counters &cnt,
+                                uint32_t &prim, PrimHit &h) {
+    const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
     if (E.iter >= OCTREE_MAX_STEPS) return kStepMiss;
-    if (E.max_dst >= 0.0f && E.t_min > E.max_dst) return kStepMiss;
+    if (max_dst >= 0.0f && E.t_min > max_dst) return kStepMiss;
     E.iter++;
     cnt.steps++;
     const v3 t_corner = vsub(vmul(E.pos, E.t_coef), E.t_bias);
@@ -418,38 +455,35 @@ __device__ inline int esvo_step(const DevScene &S, PathRay &ray, Esvo &E, uint2 
     const uint32_t cidx = E.idx ^ E.mirror;
     const bool present = (E.pmask >> cidx) & 1u;
     const bool is_leaf = (E.pmask >> (cidx + 8u)) & 1u;
-    if (present && E.t_min <= E.t_max) {
-        if (is_leaf && E.t_min >= 0.0f) {
-            const uint32_t payload = S.node_children[8u * E.parent + cidx];
-            const float cell_w = E.scale_exp2 / S.octree_scale;
-            uint32_t prim;
-            PrimHit h;
-            if (leaf_test(S, ray, payload, tc_max / S.octree_scale, cell_w, prim, h, cnt)) {
-                commit_hit(S, ray, prim, h, cnt);
-                return kStepHit;
-            }
-        } else if (!is_leaf) {
-            const float half = E.scale_exp2 * 0.5f;
-            const v3 t_center = vadd(vscale(E.t_coef, half), t_corner);
-            const float tv_max = fmn(E.t_max, tc_max);
-            if (E.t_min <= tv_max) {
-                const uint32_t child = S.node_children[8u * E.parent + cidx];
-                // validated trees never descend below the leaf level, so the slot is in [0, depth)
-                if (tc_max < E.h && E.scale >= OCTREE_MAX_SCALE - S.depth)
-                    stk_write(stk, E.scale - (OCTREE_MAX_SCALE - S.depth), E.parent, E.t_max);
-                E.h = tc_max;
-                E.parent = child;
-                E.pmask = S.node_mask[child];
-                E.scale -= 1u;
-                E.scale_exp2 = half;
-                E.idx = 0u;
-                if (t_center.x > E.t_min) { E.idx ^= 1u; E.pos.x = E.pos.x + half; }
-                if (t_center.y > E.t_min) { E.idx ^= 2u; E.pos.y = E.pos.y + half; }
-                if (t_center.z > E.t_min) { E.idx ^= 4u; E.pos.z = E.pos.z + half; }
-                E.t_max = tv_max;
-                return kStepContinue;
-            }
-        }
+    // :142-244.  Leaf (t_min >= 0) and descend (t_min <= min(t_max, tc_max)) lanes share one slot
+    // load instruction: on CDNA4 a scattered load costs the vector-memory pipe per instruction.
+    const bool live = present && E.t_min <= E.t_max;
+    const float tv_max = fmn(E.t_max, tc_max);
+    const bool take_leaf = live && is_leaf && E.t_min >= 0.0f;
+    const bool descend = live && !is_leaf && E.t_min <= tv_max;
+    uint2 slot = make_uint2(0u, 0u);
+    if (take_leaf || descend) slot = S.node_child[8u * E.parent + cidx];
+    if (take_leaf) {
+        // x / 2^-depth == x * 2^depth exactly (the oracle divides)
+        const float cell_w = E.scale_exp2 * S.inv_octree_scale;
+        if (leaf_test(S, ray, slot, tc_max * S.inv_octree_scale, cell_w, prim, h, cnt)) return kStepHit;
+    } else if (descend) {
+        const float half = E.scale_exp2 * 0.5f;
+        const v3 t_center = vadd(vscale(E.t_coef, half), t_corner);
+        // validated trees never descend below the leaf level, so the slot is in [0, depth)
+        if (tc_max < E.h && E.scale >= OCTREE_MAX_SCALE - S.depth)
+            stk_write(stk, E.scale - (OCTREE_MAX_SCALE - S.depth), E.parent, E.t_max, E.pmask);
+        E.h = tc_max;
+        E.parent = slot.x;  // (octant, its mask)
+        E.pmask = slot.y;
+        E.scale -= 1u;
+        E.scale_exp2 = half;
+        E.idx = 0u;
+        if (t_center.x > E.t_min) { E.idx ^= 1u; E.pos.x = E.pos.x + half; }
+        if (t_center.y > E.t_min) { E.idx ^= 2u; E.pos.y = E.pos.y + half; }
+        if (t_center.z > E.t_min) { E.idx ^= 4u; E.pos.z = E.pos.z + half; }
+        E.t_max = tv_max;
+        return kStepContinue;
     }
     // advance (:249-260)
     uint32_t step_mask = 0u;
@@ -470,9 +504,13 @@ __device__ inline int esvo_step(const DevScene &S, PathRay &ray, Esvo &E, uint2 
         // slots below the finest level were never written: the oracle reads its zeroed entry
         const uint32_t base = OCTREE_MAX_SCALE - S.depth;
         uint2 e = make_uint2(0u, 0u);
-        if (scale >= base) e = stk[(scale - base) * kBlock];
+        uint32_t em = S.node0_mask;
+        if (scale >= base) {
+            e = stk.e[(scale - base) * kBlock];
+            em = stk.m[(scale - base) * kBlock];
+        }
         E.parent = e.x;
-        E.pmask = S.node_mask[e.x];
+        E.pmask = em;
         E.t_max = __uint_as_float(e.y);
         const uint32_t shx = __float_as_uint(E.pos.x) >> scale;
         const uint32_t shy = __float_as_uint(E.pos.y) >> scale;
@@ -484,19 +522,10 @@ __device__ inline int esvo_step(const DevScene &S, PathRay &ray, Esvo &E, uint2 
     return kStepContinue;
 }
 
-// next_intersection prologue (path_tracer.rs:438-446) + Scene::hit direction guard (scene/mod.rs:175-179)
-__device__ __forceinline__ void begin_segment(const DevScene &S, PathRay &ray, Esvo &E, uint2 *stk) {
-    ray.prev = ray.cur;
-    const v3 d = ray.d;
-    if ((d.x == 0.0f && d.y == 0.0f && d.z == 0.0f) || isnan(d.x) || isnan(d.y) || isnan(d.z))
-        ray.d = V(0.0f, 1.0f, 0.0f);
-    esvo_begin(S, ray, E, stk);
-}
-
 // ---------------------------------------------------------------------------
 // sky + sun (scene/mod.rs:216-268, 384-426)
 // ---------------------------------------------------------------------------
-__device__ inline void sky_color(const DevSun &K, const PathRay &r, float out[3]) {
+__device__ inline void sky_color(const DevSun &K, const PathState &r, float out[3]) {
     out[0] = 0.5f; out[1] = 0.7f; out[2] = 1.0f;
     const v3 d = r.d;
     const bool textured = (r.depth == 0u) || r.specular;  // get_sky_color_interp / get_sky_color(true)
@@ -516,15 +545,14 @@ __device__ inline void sky_color(const DevSun &K, const PathRay &r, float out[3]
 // ---------------------------------------------------------------------------
 // scatter kernels (ray/mod.rs:113-373), in place: `r` becomes the next ray
 // ---------------------------------------------------------------------------
-__device__ inline void specular_reflection(PathRay &r, float roughness, uint32_t &rng) {
+__device__ inline void specular_reflection(PathState &r, float roughness) {
     const v3 n = r.n, dir = r.d;
-    r.u = r.v = 0.0f;
     r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;
     r.cur = r.prev;
     if (roughness > RAY_EPSILON) {
         const float sdot = -2.0f * vdot(dir, n);
         const v3 spec = vadd(vscale(n, sdot), dir);
-        const float x1 = rng_next(rng), x2 = rng_next(rng);
+        const float x1 = rng_next(r.rng), x2 = rng_next(r.rng);
         const float rr = sqrtf(x1), theta = 2.0f * PI_F * x2;
         float sn, cs;
         dm_sincos(theta, sn, cs);
@@ -544,11 +572,11 @@ __device__ inline void specular_reflection(PathRay &r, float roughness, uint32_t
     }
 }
 
-__device__ inline void diffuse_reflection(const DevSun &K, PathRay &r, uint32_t &rng) {
+__device__ inline void diffuse_reflection(const DevSun &K, PathState &r) {
     const v3 n = r.n;
     const v3 d_in = r.d;
     r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;  // new_from_self
-    float x1 = rng_next(rng), x2 = rng_next(rng);
+    float x1 = rng_next(r.rng), x2 = rng_next(r.rng);
     float rr = sqrtf(x1), theta = 2.0f * PI_F * x2;
     float sn, cs;
     dm_sincos(theta, sn, cs);
@@ -573,7 +601,7 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathRay &r, uint32_t 
         const float alt_rel = dm_asin(stz);
         if (alt_rel + cr > RAY_EPSILON) {
             if ((dm_hypot(stx, sty) + cr) + RAY_EPSILON < 1.0f) {
-                if (rng_next(rng) < chance) {
+                if (rng_next(r.rng) < chance) {
                     tx = stx + tx * cr;
                     ty = sty + ty * cr;
                 } else {
@@ -592,7 +620,7 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathRay &r, uint32_t 
                 const float seg = ((max_r * max_r - min_r * min_r) * cr) / PI_F;
                 chance *= seg / (cr * cr);
                 chance = fmn(chance, SUN_MAX_CHANCE);
-                if (rng_next(rng) < chance) {
+                if (rng_next(r.rng) < chance) {
                     rr = sqrtf(min_r * min_r * x1 + max_r * max_r * (1.0f - x1));
                     theta = sun_theta + (2.0f * x2 - 1.0f) * cr;
                 } else {
@@ -602,8 +630,8 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathRay &r, uint32_t 
                         if (diff >= 2.0f * PI_F) diff = diff - 2.0f * PI_F;
                         const float ad = diff > PI_F ? 2.0f * PI_F - diff : diff;
                         if (!(ad < cr)) break;
-                        x1 = rng_next(rng);
-                        x2 = rng_next(rng);
+                        x1 = rng_next(r.rng);
+                        x2 = rng_next(r.rng);
                         rr = sqrtf(x1);
                         theta = 2.0f * PI_F * x2;
                     }
@@ -631,7 +659,135 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathRay &r, uint32_t 
     }
 }
 
-enum : uint32_t { ST_IDLE = 0, ST_NEWPATH, ST_BEGIN, ST_TRAV, ST_HIT, ST_MISS, ST_FINISH, ST_DONE };
+// ---------------------------------------------------------------------------
+// path logic shared by the megakernel and the wavefront shade kernel
+// ---------------------------------------------------------------------------
+// camera ray + fresh path (camera.rs:77-86, tile_renderer.rs:695-703)
+__device__ inline void new_path(const DevCamera &C, const DevRender &R, uint32_t pix, uint32_t sample, PathState &ps) {
+    const uint32_t x = pix % R.W, y = pix / R.W;
+    ps.rng = path_state(R.seed, pix, sample);
+    const float jlo = -1.0f / R.dim, jhi = 1.0f / R.dim;
+    const float xn = ((float)(2u * x + 1u) - (float)R.W) / R.dim;
+    const float yn = ((float)(2u * (R.H - y) - 1u) - (float)R.H) / R.dim;
+    const float dx = jlo + (jhi - jlo) * rng_next(ps.rng);
+    const float dy = jlo + (jhi - jlo) * rng_next(ps.rng);
+    const v3 nd = vadd(vadd(vscale(V(C.dir[0], C.dir[1], C.dir[2]), C.d_factor),
+                            vscale(V(C.right[0], C.right[1], C.right[2]), xn + dx)),
+                       vscale(V(C.up[0], C.up[1], C.up[2]), yn + dy));
+    ps.o = V(C.eye[0], C.eye[1], C.eye[2]);
+    ps.d = vnorm(nd);
+    ps.n = V(0.0f, 0.0f, 0.0f);
+    ps.col[0] = ps.col[1] = ps.col[2] = ps.col[3] = 0.0f;
+    ps.T = V(1.0f, 1.0f, 1.0f);
+    ps.L = V(0.0f, 0.0f, 0.0f);
+    ps.cur = ps.prev = ps.depth = 0u;
+    ps.last_prim = kPrimNone;
+    ps.path_segs = 0u;
+    ps.specular = true;
+}
+
+// next_intersection prologue (path_tracer.rs:438-446) + Scene::hit direction guard
+// (scene/mod.rs:175-179) + the per-path segment cap [C15]. false = the path ends here.
+__device__ __forceinline__ bool begin_segment(PathState &ps) {
+    if (ps.path_segs >= MAX_PATH_SEGMENTS) return false;
+    ps.path_segs++;
+    ps.prev = ps.cur;
+    const v3 d = ps.d;
+    if ((d.x == 0.0f && d.y == 0.0f && d.z == 0.0f) || isnan(d.x) || isnan(d.y) || isnan(d.z))
+        ps.d = V(0.0f, 1.0f, 0.0f);
+    return true;
+}
+
+__device__ __forceinline__ TraceRay trace_ray_of(const DevScene &S, const PathState &ps) {
+    return make_trace_ray(S, ps.o, ps.d, ps.last_prim, vdot(ps.d, ps.n) < 0.0f);
+}
+
+// path_tracer.rs:15-135 in forward-throughput form, from a finished segment to either the
+// next segment's ray (returns true) or the end of the path (returns false).
+__device__ inline bool shade_segment(const DevScene &S, const DevRender &R, PathState &ray, bool hit,
+                                     Counters &cnt) {
+    if (!hit) {
+        float sky[3];
+        sky_color(S.sun, ray, sky);
+        ray.L = V(ray.L.x + ray.T.x * sky[0], ray.L.y + ray.T.y * sky[1], ray.L.z + ray.T.z * sky[2]);
+        return false;
+    }
+    const DevMaterial m = S.mats[ray.cur];
+    const float ior2 = S.mats[ray.prev].ior;
+    const float specular = m.specular, diffuse = ray.col[3], absorb = ray.col[3];
+    const float ior1 = m.ior;
+    if (ray.col[3] + specular < RAY_EPSILON && ior1 == ior2) {  // [C4]
+        ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
+        return true;
+    }
+    if (ray.depth + 1u >= R.max_depth) return false;
+    ray.depth += 1u;
+    cnt.shade++;
+    v3 &T = ray.T;
+    const float metal = m.metalness;
+    const bool do_metal = metal > RAY_EPSILON && rng_next(ray.rng) < metal;
+    if (do_metal || (specular > RAY_EPSILON && rng_next(ray.rng) < specular)) {
+        if (do_metal) T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
+        specular_reflection(ray, m.roughness);
+    } else if (rng_next(ray.rng) < diffuse) {
+        if (S.emitters && m.emittance > RAY_EPSILON) {
+            const v3 e = V(ray.col[0] * ray.col[0] * m.emittance, ray.col[1] * ray.col[1] * m.emittance,
+                           ray.col[2] * ray.col[2] * m.emittance);
+            ray.L = V(ray.L.x + T.x * e.x, ray.L.y + T.y * e.y, ray.L.z + T.z * e.z);
+        }
+        T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
+        diffuse_reflection(S.sun, ray);
+    } else if (fabsf(ior1 - ior2) >= RAY_EPSILON) {
+        // do_refraction (path_tracer.rs:318-401) [C14]
+        const bool refr = (m.flags & MAT_FLAG_REFRACTIVE) != 0u;
+        const float n1n2 = ior1 / ior2;
+        const float cos_theta = -vdot(ray.d, ray.n);
+        const float radicand = 1.0f - n1n2 * n1n2 * (1.0f - cos_theta * cos_theta);
+        if (refr && radicand < RAY_EPSILON) {
+            specular_reflection(ray, m.roughness);
+        } else {
+            const float a = n1n2 - 1.0f, b = n1n2 + 1.0f;
+            const float r0 = a * a / (b * b);
+            const float cc = 1.0f - cos_theta;
+            const float c5 = ((cc * cc) * (cc * cc)) * cc;
+            const float rtheta = r0 + (1.0f - r0) * c5;
+            if (rng_next(ray.rng) < rtheta) {
+                specular_reflection(ray, m.roughness);
+            } else {
+                T = V(T.x * (ray.col[0] * absorb), T.y * (ray.col[1] * absorb), T.z * (ray.col[2] * absorb));
+                const v3 d_in = ray.d, n = ray.n;
+                ray.col[0] = ray.col[1] = ray.col[2] = ray.col[3] = 0.0f;
+                if (refr) {
+                    const float t2 = sqrtf(radicand);
+                    v3 d;
+                    if (cos_theta > 0.0f) d = vadd(vscale(d_in, n1n2), vscale(n, n1n2 * cos_theta - t2));
+                    else d = vsub(vscale(d_in, n1n2), vscale(n, -n1n2 * cos_theta - t2));
+                    ray.d = vnorm(d);
+                    if (signum_(vdot(n, ray.d)) != signum_(vdot(n, d_in))) {
+                        const float factor = signum_(vdot(n, d_in)) * -RAY_EPSILON - vdot(ray.d, n);
+                        ray.d = vnorm(vadd(ray.d, vscale(n, factor)));
+                    }
+                    ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
+                }
+            }
+        }
+    } else {
+        // do_transmission (path_tracer.rs:403-422)
+        T = V(T.x * (ray.col[0] * absorb), T.y * (ray.col[1] * absorb), T.z * (ray.col[2] * absorb));
+        ray.col[0] = ray.col[1] = ray.col[2] = ray.col[3] = 0.0f;
+        ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
+    }
+    return true;
+}
+
+// running mean of render_tile_average (tile_renderer.rs:716-733), branch_count = 1
+__device__ __forceinline__ void running_mean(float4 &fb, v3 c, uint32_t spp) {
+    const float s_inv = 1.0f / (float)(1u + spp);
+    const float fs = (float)spp;
+    fb.x = (fb.x * fs + c.x * 1.0f) * s_inv;
+    fb.y = (fb.y * fs + c.y * 1.0f) * s_inv;
+    fb.z = (fb.z * fs + c.z * 1.0f) * s_inv;
+}
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -650,49 +806,59 @@ __device__ inline unsigned long long wave_sum(uint32_t v) {
     return s;
 }
 
+__device__ inline void flush_counters(const Counters &cnt, unsigned long long *stats) {
+    const uint32_t vals[kStatCount] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};
+#pragma unroll
+    for (int i = 0; i < kStatCount; ++i) {
+        const unsigned long long s = wave_sum(vals[i]);
+        if ((threadIdx.x & 63u) == 0u && s) atomicAdd(&stats[i], s);
+    }
+}
+
+// wave-aggregated atomic ticket: each lane with `want` gets a distinct value from *ctr
+__device__ __forceinline__ uint32_t wave_ticket(uint32_t *ctr, bool want) {
+    const uint64_t m = __ballot(want);
+    if (m == 0ull) return 0u;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    uint32_t base = 0u;
+    if ((threadIdx.x & 63u) == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    return base + lanes_below(m);
+}
+
+// ===========================================================================
+// megakernel (kept for A/B: OCTPT_RENDER_MEGAKERNEL)
+// ===========================================================================
+enum : uint32_t { ST_IDLE = 0, ST_NEWPATH, ST_BEGIN, ST_TRAV, ST_HIT, ST_MISS, ST_FINISH, ST_DONE };
+
 __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C, DevRender R, float4 *__restrict__ accum,
                                                         uint32_t *__restrict__ segcount, uint32_t *__restrict__ counter,
                                                         unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
-    uint2 *stk = lds_stack + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u;
-    const v3 cam_eye = V(C.eye[0], C.eye[1], C.eye[2]);
-    const v3 cam_dir = V(C.dir[0], C.dir[1], C.dir[2]);
-    const v3 cam_right = V(C.right[0], C.right[1], C.right[2]);
-    const v3 cam_up = V(C.up[0], C.up[1], C.up[2]);
-    const float jlo = -1.0f / R.dim, jhi = 1.0f / R.dim;
-
+    const Stack stk = stack_of(lds_stack, S.depth);
     uint32_t state = ST_IDLE;
-    uint32_t item = 0u, pix = 0u, k = 0u, pix_segs = 0u, path_segs = 0u, acc_idx = 0u;
+    uint32_t pix = 0u, k = 0u, pix_segs = 0u, acc_idx = 0u;
     float4 fb = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-    PathRay ray;
-    ray.cur = ray.prev = ray.depth = 0u;
-    ray.last_prim = kPrimNone;
-    ray.specular = true;
-    v3 T = V(1.0f, 1.0f, 1.0f), L = V(0.0f, 0.0f, 0.0f);
-    uint32_t rng = 0u;
+    PathState ray;
+    TraceRay tr;
     Esvo E;
+    uint32_t hprim = kPrimNone;
+    PrimHit hh;
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
 
     for (;;) {
-        // --- refill: lanes without a pixel take the next work items (one atomic per wave)
-        const uint64_t need = __ballot(state == ST_IDLE);
-        if (need) {
-            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need) - 1u;
-            uint32_t base = 0u;
-            if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(need));
-            base = __shfl(base, (int)leader);
-            if (state == ST_IDLE) {
-                const uint32_t my = base + lanes_below(need);
+        const bool need = state == ST_IDLE;
+        if (__ballot(need)) {
+            const uint32_t my = wave_ticket(counter, need);
+            if (need) {
                 if (my >= R.total_items) {
                     state = ST_DONE;
                 } else {
                     uint32_t x, y;
                     item_pixel(R, my, x, y);
                     if (x < R.W && y < R.H) {
-                        item = my;
                         pix = y * R.W + x;
-                        acc_idx = R.compact ? item : pix;
+                        acc_idx = R.compact ? my : pix;
                         fb = accum[acc_idx];
                         k = 0u;
                         pix_segs = 0u;
@@ -702,144 +868,47 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             }
         }
         if (__ballot(state != ST_DONE) == 0ull) break;
-
-        // --- camera ray (camera.rs:77-86, tile_renderer.rs:695-703)
         if (state == ST_NEWPATH) {
-            const uint32_t x = pix % R.W, y = pix / R.W;
-            rng = path_state(R.seed, pix, R.spp_start + k);
-            const float xn = ((float)(2u * x + 1u) - (float)R.W) / R.dim;
-            const float yn = ((float)(2u * (R.H - y) - 1u) - (float)R.H) / R.dim;
-            const float dx = jlo + (jhi - jlo) * rng_next(rng);
-            const float dy = jlo + (jhi - jlo) * rng_next(rng);
-            const v3 nd = vadd(vadd(vscale(cam_dir, C.d_factor), vscale(cam_right, xn + dx)), vscale(cam_up, yn + dy));
-            ray.o = cam_eye;
-            ray.d = vnorm(nd);
-            ray.n = V(0.0f, 0.0f, 0.0f);
-            ray.cur = ray.prev = ray.depth = 0u;
-            ray.last_prim = kPrimNone;
-            ray.specular = true;
-            T = V(1.0f, 1.0f, 1.0f);
-            L = V(0.0f, 0.0f, 0.0f);
-            path_segs = 0u;
+            new_path(C, R, pix, R.spp_start + k, ray);
             cnt.paths++;
             state = ST_BEGIN;
         }
         if (state == ST_BEGIN) {
-            if (path_segs >= MAX_PATH_SEGMENTS) {
-                state = ST_FINISH;  // [C15]: the path ends without further contribution
-            } else {
-                begin_segment(S, ray, E, stk);
+            if (begin_segment(ray)) {
+                tr = trace_ray_of(S, ray);
+                esvo_begin(S, tr, E, stk);
                 cnt.segs++;
                 pix_segs++;
-                path_segs++;
                 state = ST_TRAV;
+            } else {
+                state = ST_FINISH;
             }
         }
-
-        // --- traversal: keep stepping while at least half of the live lanes traverse
-        {
-            bool first = true;
-            for (;;) {
-                const uint64_t tm = __ballot(state == ST_TRAV);
-                if (tm == 0ull) break;
-                if (!first) {
-                    const uint64_t am = __ballot(state != ST_DONE);
-                    if (2u * (uint32_t)__popcll(tm) < (uint32_t)__popcll(am)) break;
-                }
-                first = false;
-                if (state == ST_TRAV) {
-                    const int rs = esvo_step(S, ray, E, stk, cnt);
-                    if (rs == kStepHit) state = ST_HIT;
-                    else if (rs == kStepMiss) state = ST_MISS;
-                }
+        bool first = true;
+        for (;;) {  // keep stepping while at least half of the live lanes traverse
+            const uint64_t tm = __ballot(state == ST_TRAV);
+            if (tm == 0ull) break;
+            if (!first) {
+                const uint64_t am = __ballot(state != ST_DONE);
+                if (2u * (uint32_t)__popcll(tm) < (uint32_t)__popcll(am)) break;
+            }
+            first = false;
+            if (state == ST_TRAV) {
+                const int rs = esvo_step(S, tr, E, stk, cnt, hprim, hh);
+                if (rs == kStepHit) state = ST_HIT;
+                else if (rs == kStepMiss) state = ST_MISS;
             }
         }
-
-        // --- shading (path_tracer.rs:15-135 in forward-throughput form)
         if (state == ST_HIT || state == ST_MISS || state == ST_FINISH) {
-            bool path_done = state == ST_FINISH;
-            if (state == ST_MISS) {
-                float sky[3];
-                sky_color(S.sun, ray, sky);
-                L = V(L.x + T.x * sky[0], L.y + T.y * sky[1], L.z + T.z * sky[2]);
-                path_done = true;
-            } else if (state == ST_HIT) {
-                const DevMaterial m = S.mats[ray.cur];
-                const float ior2 = S.mats[ray.prev].ior;
-                const float specular = m.specular, diffuse = ray.col[3], absorb = ray.col[3];
-                const float ior1 = m.ior;
-                if (ray.col[3] + specular < RAY_EPSILON && ior1 == ior2) {  // [C4]
-                    ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
-                    state = ST_BEGIN;
-                } else if (ray.depth + 1u >= R.max_depth) {
-                    path_done = true;
-                } else {
-                    ray.depth += 1u;
-                    cnt.shade++;
-                    const float metal = m.metalness;
-                    const bool do_metal = metal > RAY_EPSILON && rng_next(rng) < metal;
-                    if (do_metal || (specular > RAY_EPSILON && rng_next(rng) < specular)) {
-                        if (do_metal) T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
-                        specular_reflection(ray, m.roughness, rng);
-                    } else if (rng_next(rng) < diffuse) {
-                        if (S.emitters && m.emittance > RAY_EPSILON) {
-                            const v3 e = V(ray.col[0] * ray.col[0] * m.emittance, ray.col[1] * ray.col[1] * m.emittance,
-                                           ray.col[2] * ray.col[2] * m.emittance);
-                            L = V(L.x + T.x * e.x, L.y + T.y * e.y, L.z + T.z * e.z);
-                        }
-                        T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
-                        diffuse_reflection(S.sun, ray, rng);
-                    } else if (fabsf(ior1 - ior2) >= RAY_EPSILON) {
-                        // do_refraction (path_tracer.rs:318-401) [C14]
-                        const bool refr = (m.flags & MAT_FLAG_REFRACTIVE) != 0u;
-                        const float n1n2 = ior1 / ior2;
-                        const float cos_theta = -vdot(ray.d, ray.n);
-                        const float radicand = 1.0f - n1n2 * n1n2 * (1.0f - cos_theta * cos_theta);
-                        if (refr && radicand < RAY_EPSILON) {
-                            specular_reflection(ray, m.roughness, rng);
-                        } else {
-                            const float a = n1n2 - 1.0f, b = n1n2 + 1.0f;
-                            const float r0 = a * a / (b * b);
-                            const float cc = 1.0f - cos_theta;
-                            const float c5 = ((cc * cc) * (cc * cc)) * cc;
-                            const float rtheta = r0 + (1.0f - r0) * c5;
-                            if (rng_next(rng) < rtheta) {
-                                specular_reflection(ray, m.roughness, rng);
-                            } else {
-                                T = V(T.x * (ray.col[0] * absorb), T.y * (ray.col[1] * absorb), T.z * (ray.col[2] * absorb));
-                                const v3 d_in = ray.d, n = ray.n;
-                                ray.col[0] = ray.col[1] = ray.col[2] = ray.col[3] = 0.0f;
-                                if (refr) {
-                                    const float t2 = sqrtf(radicand);
-                                    v3 d;
-                                    if (cos_theta > 0.0f) d = vadd(vscale(d_in, n1n2), vscale(n, n1n2 * cos_theta - t2));
-                                    else d = vsub(vscale(d_in, n1n2), vscale(n, -n1n2 * cos_theta - t2));
-                                    ray.d = vnorm(d);
-                                    if (signum_(vdot(n, ray.d)) != signum_(vdot(n, d_in))) {
-                                        const float factor = signum_(vdot(n, d_in)) * -RAY_EPSILON - vdot(ray.d, n);
-                                        ray.d = vnorm(vadd(ray.d, vscale(n, factor)));
-                                    }
-                                    ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
-                                }
-                            }
-                        }
-                    } else {
-                        // do_transmission (path_tracer.rs:403-422)
-                        T = V(T.x * (ray.col[0] * absorb), T.y * (ray.col[1] * absorb), T.z * (ray.col[2] * absorb));
-                        ray.col[0] = ray.col[1] = ray.col[2] = ray.col[3] = 0.0f;
-                        ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
-                    }
-                    state = ST_BEGIN;
-                }
+            bool cont = false;
+            if (state != ST_FINISH) {
+                if (state == ST_HIT) commit_hit(S, ray, hprim, hh, cnt);
+                cont = shade_segment(S, R, ray, state == ST_HIT, cnt);
             }
-            if (path_done) {
-                // running mean of render_tile_average (tile_renderer.rs:716-733), branch_count = 1
-                const uint32_t spp = R.spp_start + k;
-                const float s_inv = 1.0f / (float)(1u + spp);
-                const float fs = (float)spp;
-                fb.x = (fb.x * fs + L.x * 1.0f) * s_inv;
-                fb.y = (fb.y * fs + L.y * 1.0f) * s_inv;
-                fb.z = (fb.z * fs + L.z * 1.0f) * s_inv;
+            if (cont) {
+                state = ST_BEGIN;
+            } else {
+                running_mean(fb, ray.L, R.spp_start + k);
                 k++;
                 if (k < R.spp_count) {
                     state = ST_NEWPATH;
@@ -851,14 +920,220 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             }
         }
     }
+    flush_counters(cnt, stats);
+}
 
-    // --- statistics: one 64-bit atomic per counter per wave
-    const uint32_t vals[kStatCount] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};
-#pragma unroll
-    for (int i = 0; i < kStatCount; ++i) {
-        const unsigned long long s = wave_sum(vals[i]);
-        if (lane == 0u && s) atomicAdd(&stats[i], s);
+// ===========================================================================
+// wavefront path tracer: seed -> (extend -> shade)* -> resolve
+// ===========================================================================
+// Records (16 bytes each).  Ray records live at their queue position, so extend reads them
+// without an indirection; the path state lives at its slot:
+//   ray0[q][i] = (o.xyz, last_prim)   ray1[q][i] = (d.xyz, slot | self_inward << 31)
+//   hit[i]     = (prim, t, inside | axis<<1 | (nsgn<0)<<3, -)
+//   pa[slot]   = (T.xyz, L.x)  pb[slot] = (L.y, L.z, rng, item)  pc[slot] = (cur_mat, depth | spec<<8 | segs<<16)
+__device__ __forceinline__ void store_ray(const WaveBuffers &B, uint32_t q, uint32_t pos, uint32_t slot,
+                                          const PathState &ps) {
+    B.ray0[q][pos] = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.last_prim));
+    B.ray1[q][pos] = make_float4(ps.d.x, ps.d.y, ps.d.z,
+                                 __uint_as_float(slot | (vdot(ps.d, ps.n) < 0.0f ? 0x80000000u : 0u)));
+}
+
+__device__ __forceinline__ void store_path(const WaveBuffers &B, uint32_t slot, const PathState &ps, uint32_t item) {
+    B.pa[slot] = make_float4(ps.T.x, ps.T.y, ps.T.z, ps.L.x);
+    B.pb[slot] = make_float4(ps.L.y, ps.L.z, __uint_as_float(ps.rng), __uint_as_float(item));
+    B.pc[slot] = make_uint2(ps.cur, ps.depth | (ps.specular ? 1u << 8 : 0u) | (ps.path_segs << 16));
+}
+
+__device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, float4 r0, float4 r1, PathState &ps,
+                                          uint32_t &item) {
+    const float4 a = B.pa[slot], b = B.pb[slot];
+    const uint2 c = B.pc[slot];
+    ps.o = V(r0.x, r0.y, r0.z);
+    ps.last_prim = __float_as_uint(r0.w);
+    ps.d = V(r1.x, r1.y, r1.z);
+    ps.T = V(a.x, a.y, a.z);
+    ps.L = V(a.w, b.x, b.y);
+    ps.rng = __float_as_uint(b.z);
+    item = __float_as_uint(b.w);
+    ps.cur = c.x;
+    ps.prev = c.x;  // begin_segment set prev = cur before this segment was traced
+    ps.depth = c.y & 255u;
+    ps.specular = (c.y >> 8) & 1u;
+    ps.path_segs = c.y >> 16;
+}
+
+// generate the path of chunk item `item` into `slot`; false when the pixel lies outside the image
+__device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t slot,
+                                 uint32_t item, PathState &ps, Counters &cnt) {
+    const uint32_t px_item = item % R.total_items, s_local = item / R.total_items;
+    uint32_t x, y;
+    item_pixel(R, px_item, x, y);
+    if (x >= R.W || y >= R.H) {
+        B.color[item] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        return false;
     }
+    new_path(C, R, y * R.W + x, R.spp_start + s_local, ps);
+    begin_segment(ps);  // first segment: never capped
+    cnt.paths++;
+    store_path(B, slot, ps, item);
+    return true;
+}
+
+// lanes with `want` start the next chunk items in their slots; items whose pixel lies outside
+// the image are consumed (zero colour) and the lane draws again, so a slot only goes idle
+// once the chunk has no items left.  Every lane of the wave must call this.
+__device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t slot, bool want,
+                             uint32_t chunk_items, PathState &ps, Counters &cnt) {
+    bool need = want, ok = false;
+    while (__ballot(need) != 0ull) {
+        const uint32_t ni = wave_ticket(&B.ctrl->next_item, need);
+        if (need) {
+            if (ni >= chunk_items) {
+                need = false;
+            } else if (seed_item(C, R, B, slot, ni, ps, cnt)) {
+                ok = true;
+                need = false;
+            }
+        }
+    }
+    return ok;
+}
+
+__global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender R, WaveBuffers B, uint32_t n_seed,
+                                                         uint32_t chunk_items, unsigned long long *__restrict__ stats) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    PathState ps;
+    const bool ok = regen(C, R, B, i, i < n_seed, chunk_items, ps, cnt);
+    const uint32_t pos = wave_ticket(&B.ctrl->count[0], ok);
+    if (ok) store_ray(B, 0u, pos, i, ps);
+    flush_counters(cnt, stats);
+}
+
+// extend: closest-hit queries for every queued ray.  Persistent waves; a lane that finishes
+// its ray idles until at least `refill` lanes of the wave are idle, then the wave pulls that
+// many rays from the queue with one atomic (Aila & Laine dynamic fetch).
+#ifndef OCTPT_EXTEND_WAVES
+#define OCTPT_EXTEND_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
+                                                           unsigned long long *__restrict__ stats) {
+    extern __shared__ uint2 lds_stack[];
+    const Stack stk = stack_of(lds_stack, S.depth);
+    const uint32_t count = B.ctrl->count[q];
+    const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the other queue is refilled by this iteration's shade
+        B.ctrl->count[q ^ 1u] = 0u;
+        B.ctrl->head[q ^ 1u] = 0u;
+    }
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    bool active = false, done = false;
+    uint32_t pos = 0u;
+    TraceRay tr;
+    Esvo E;
+    for (;;) {
+        const bool idle = !active && !done;
+        const uint64_t im = __ballot(idle);
+        if (im != 0ull && ((uint32_t)__popcll(im) >= refill || __ballot(active) == 0ull)) {
+            const uint32_t my = wave_ticket(&B.ctrl->head[q], idle);
+            if (idle) {
+                if (my < count) {
+                    pos = my;
+                    const float4 r0 = ray0[my], r1 = ray1[my];
+                    tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
+                                        (__float_as_uint(r1.w) >> 31) != 0u);
+                    esvo_begin(S, tr, E, stk);
+                    cnt.segs++;
+                    active = true;
+                } else {
+                    done = true;
+                }
+            }
+        }
+        if (__ballot(active) == 0ull) break;
+        if (active) {
+            uint32_t prim = kPrimNone;
+            PrimHit h;
+            const int rs = esvo_step(S, tr, E, stk, cnt, prim, h);
+            if (rs != kStepContinue) {
+                uint4 rec = make_uint4(kPrimNone, 0u, 0u, 0u);
+                if (rs == kStepHit)
+                    rec = make_uint4(prim, __float_as_uint(h.t),
+                                     h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u), 0u);
+                B.hit[pos] = rec;
+                active = false;
+            }
+        }
+    }
+    flush_counters(cnt, stats);
+}
+
+// shade: one lane per traced ray (grid-stride, wave-uniform trip count)
+__global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, DevCamera C, DevRender R, WaveBuffers B,
+                                                          uint32_t q, uint32_t chunk_items,
+                                                          unsigned long long *__restrict__ stats) {
+    const uint32_t count = B.ctrl->count[q];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    for (uint32_t base = wave * 64u; base < count; base += n_waves * 64u) {
+        const uint32_t i = base + lane;
+        const bool valid = i < count;
+        uint32_t slot = 0u, item = 0u;
+        bool append = false, finished = false;
+        PathState ps;
+        if (valid) {
+            const float4 r0 = B.ray0[q][i], r1 = B.ray1[q][i];
+            slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
+            load_path(B, slot, r0, r1, ps, item);
+            const uint4 hr = B.hit[i];
+            const bool hit = hr.x != kPrimNone;
+            if (hit) {
+                PrimHit h;
+                h.t = __uint_as_float(hr.y);
+                h.inside = hr.z & 1u;
+                h.axis = (hr.z >> 1) & 3u;
+                h.nsgn = (hr.z & 8u) ? -1.0f : 1.0f;
+                ps.n = V(0.0f, 0.0f, 0.0f);
+                commit_hit(S, ps, hr.x, h, cnt);
+            }
+            bool cont = shade_segment(S, R, ps, hit, cnt);
+            if (cont) cont = begin_segment(ps);
+            if (cont) {
+                store_path(B, slot, ps, item);
+                append = true;
+            } else {
+                B.color[item] = make_float4(ps.L.x, ps.L.y, ps.L.z, __uint_as_float(ps.path_segs));
+                finished = true;
+            }
+        }
+        // regenerate: finished lanes take the next chunk items (path regeneration)
+        if (regen(C, R, B, slot, finished, chunk_items, ps, cnt)) append = true;
+        const uint32_t pos = wave_ticket(&B.ctrl->count[q ^ 1u], append);
+        if (append) store_ray(B, q ^ 1u, pos, slot, ps);
+    }
+    flush_counters(cnt, stats);
+}
+
+// resolve: per pixel, the chunk's samples in sample order into the running mean
+__global__ __launch_bounds__(kBlock) void wf_resolve_kernel(DevRender R, WaveBuffers B, uint32_t chunk_spp,
+                                                            float4 *__restrict__ accum, uint32_t *__restrict__ segcount) {
+    const uint32_t px_item = blockIdx.x * kBlock + threadIdx.x;
+    if (px_item >= R.total_items) return;
+    uint32_t x, y;
+    item_pixel(R, px_item, x, y);
+    if (x >= R.W || y >= R.H) return;
+    const uint32_t acc_idx = R.compact ? px_item : y * R.W + x;
+    float4 fb = accum[acc_idx];
+    uint32_t segs = 0u;
+    for (uint32_t s = 0; s < chunk_spp; ++s) {
+        const float4 c = B.color[(size_t)s * R.total_items + px_item];
+        running_mean(fb, V(c.x, c.y, c.z), R.spp_start + s);
+        segs += __float_as_uint(c.w);
+    }
+    accum[acc_idx] = fb;
+    if (segcount) segcount[acc_idx] += segs;
 }
 
 // one ray per thread closest-hit query (Scene::hit) for octpt_intersect
@@ -868,30 +1143,34 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
                                                            float *__restrict__ out_t, uint32_t *__restrict__ out_prim,
                                                            float *__restrict__ out_normal, uint32_t *__restrict__ out_steps) {
     extern __shared__ uint2 lds_stack[];
-    uint2 *stk = lds_stack + threadIdx.x;
+    const Stack stk = stack_of(lds_stack, S.depth);
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    PathRay ray;
-    ray.o = V(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
-    ray.d = V(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
-    ray.n = last_normal ? V(last_normal[3 * i], last_normal[3 * i + 1], last_normal[3 * i + 2]) : V(0.0f, 0.0f, 0.0f);
-    ray.cur = ray.prev = ray.depth = 0u;
-    ray.last_prim = last_prim ? last_prim[i] : kPrimNone;
-    ray.specular = true;
+    PathState ps;
+    ps.o = V(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+    ps.d = V(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+    ps.n = last_normal ? V(last_normal[3 * i], last_normal[3 * i + 1], last_normal[3 * i + 2]) : V(0.0f, 0.0f, 0.0f);
+    ps.cur = ps.prev = ps.depth = 0u;
+    ps.last_prim = last_prim ? last_prim[i] : kPrimNone;
+    ps.specular = true;
+    const TraceRay tr = trace_ray_of(S, ps);
     Esvo E;
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    esvo_begin(S, ray, E, stk);
+    esvo_begin(S, tr, E, stk);
+    uint32_t prim = kPrimNone;
+    PrimHit h;
     int rs;
     do {
-        rs = esvo_step(S, ray, E, stk, cnt);
+        rs = esvo_step(S, tr, E, stk, cnt, prim, h);
     } while (rs == kStepContinue);
     if (rs == kStepHit) {
-        out_t[i] = ray.t;
-        out_prim[i] = ray.last_prim;
+        commit_hit(S, ps, prim, h, cnt);
+        out_t[i] = h.t;
+        out_prim[i] = prim;
         if (out_normal) {
-            out_normal[3 * i] = ray.n.x;
-            out_normal[3 * i + 1] = ray.n.y;
-            out_normal[3 * i + 2] = ray.n.z;
+            out_normal[3 * i] = ps.n.x;
+            out_normal[3 * i + 1] = ps.n.y;
+            out_normal[3 * i + 2] = ps.n.z;
         }
     } else {
         out_t[i] = __int_as_float(0x7f800000);
@@ -924,7 +1203,7 @@ __global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t N, const float4 
 
 }  // namespace
 
-size_t render_lds_bytes(uint32_t depth) { return (size_t)depth * kBlock * sizeof(uint2); }
+size_t render_lds_bytes(uint32_t depth) { return (size_t)depth * kBlock * (sizeof(uint2) + sizeof(uint16_t)); }
 
 int render_blocks_per_cu(uint32_t depth) {
     int blocks = 0;
@@ -934,10 +1213,45 @@ int render_blocks_per_cu(uint32_t depth) {
     return blocks > 0 ? blocks : 1;
 }
 
+int extend_blocks_per_cu(uint32_t depth) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void *>(wf_extend_kernel), kBlock,
+                                                     render_lds_bytes(depth)) != hipSuccess)
+        return 1;
+    return blocks > 0 ? blocks : 1;
+}
+
 hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum, uint32_t *segcount,
                          uint32_t *counter, unsigned long long *stats, int grid, hipStream_t stream) {
     hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R, accum,
                        segcount, counter, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t n_seed,
+                          uint32_t chunk_items, unsigned long long *stats, hipStream_t stream) {
+    hipLaunchKernelGGL(wf_seed_kernel, dim3((n_seed + kBlock - 1u) / kBlock), dim3(kBlock), 0, stream, C, R, B, n_seed,
+                       chunk_items, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
+                            unsigned long long *stats, hipStream_t stream) {
+    hipLaunchKernelGGL(wf_extend_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, B, q, refill,
+                       stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
+                           uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream) {
+    hipLaunchKernelGGL(wf_shade_kernel, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,
+                             uint32_t *segcount, hipStream_t stream) {
+    hipLaunchKernelGGL(wf_resolve_kernel, dim3((R.total_items + kBlock - 1u) / kBlock), dim3(kBlock), 0, stream, R, B,
+                       chunk_spp, accum, segcount);
     return hipGetLastError();
 }
 

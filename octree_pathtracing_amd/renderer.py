@@ -45,10 +45,10 @@ class FrameInFlight:
         self._spp_after = spp_after
         self._done = False
 
-    def _finish(self):
+    def _finish(self, cancelled: bool = False):
         if not self._done:
             self._done = True
-            self._r._frame_done(self)
+            self._r._frame_done(self, cancelled)
             self._r._lib.octpt_frame_release(self._h)
 
     def poll(self):
@@ -58,7 +58,7 @@ class FrameInFlight:
         if st == _lib.NOT_READY:
             return FrameInFlightPoll.NotReady, self
         if st == _lib.CANCELLED:
-            self._finish()
+            self._finish(cancelled=True)
             return FrameInFlightPoll.Cancelled, None
         _lib.check(lib, self._r._ctx, st)
         self._finish()
@@ -69,7 +69,7 @@ class FrameInFlight:
         lib = self._r._lib
         st = lib.octpt_frame_wait(self._h)
         if st == _lib.CANCELLED:
-            self._finish()
+            self._finish(cancelled=True)
             raise _lib.OctptError(st, "frame cancelled")
         _lib.check(lib, self._r._ctx, st)
         self._finish()
@@ -184,8 +184,9 @@ class HipRenderer:
         self._in_flight = f
         return f
 
-    def _frame_done(self, f: FrameInFlight):
-        self._spp = f._spp_after
+    def _frame_done(self, f: FrameInFlight, cancelled: bool = False):
+        if not cancelled:  # a cancelled frame leaves the accumulation untouched
+            self._spp = f._spp_after
         self._in_flight = None
         self._status = RendererStatus.Stopped
 
@@ -204,9 +205,11 @@ class HipRenderer:
         return self._accum
 
     # ------------------------------------------------------------ direct entry points
-    def params(self, W, H, spp_start, spp_count, shard_index=0, shard_count=1, compact=False) -> "_lib.RenderParams":
+    def params(self, W, H, spp_start, spp_count, shard_index=0, shard_count=1, compact=False,
+               megakernel=False) -> "_lib.RenderParams":
+        flags = (_lib.RENDER_SHARD_COMPACT if compact else 0) | (_lib.RENDER_MEGAKERNEL if megakernel else 0)
         return _lib.RenderParams(W, H, spp_start, spp_count, self.max_depth, 1, self.seed, shard_index, shard_count,
-                                 _lib.RENDER_SHARD_COMPACT if compact else 0)
+                                 flags)
 
     def render(self, settings: RenderSettings, accum: np.ndarray | None = None, spp_start: int = 0,
                with_rgba: bool = False):

@@ -10,9 +10,10 @@ r = HipRenderer(0)
 r.set_scene(sc); r.set_camera(cam)
 W, H = rs.width, rs.height
 acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"); acc[:, 3] = 1
-for spp in [int(x) for x in (sys.argv[2:] or ["4", "16", "64", "256"])]:
+mega = "--mega" in sys.argv
+for spp in [int(x) for x in (a for a in sys.argv[2:] if not a.startswith("--"))] or [4, 16, 64, 256]:
     r.reset_stats()
-    p = r.params(W, H, 0, spp)
+    p = r.params(W, H, 0, spp, megakernel=mega)
     torch.cuda.synchronize(); t = time.perf_counter()
     r.render_device(p, acc.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize(); dt = time.perf_counter() - t

@@ -38,7 +38,7 @@ def rel_err(a, b):
     return np.abs(a - b) / np.maximum(np.abs(b), 1e-3)
 
 
-def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), compact=False):
+def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), compact=False, megakernel=False):
     """Device render through octpt_render_device; returns (accum[H,W,4] or compact, seg_count, stats)."""
     from octree_pathtracing_amd.renderer import shard_pixels
 
@@ -54,7 +54,7 @@ def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), com
     else:
         acc = torch.as_tensor(accum.reshape(-1, 4), device="cuda").clone()
     segs = torch.zeros(n, dtype=torch.int32, device="cuda")
-    p = r.params(W, H, spp_start, rs.spp, shard[0], shard[1], compact)
+    p = r.params(W, H, spp_start, rs.spp, shard[0], shard[1], compact, megakernel)
     stream = torch.cuda.current_stream().cuda_stream
     r.render_device(p, acc.data_ptr(), segs.data_ptr(), stream)
     torch.cuda.synchronize()
@@ -205,10 +205,14 @@ def test_async_frame_and_cancel(renderer):
     sync, rgba = renderer.render(rs, with_rgba=True)
     assert np.array_equal(payload, rgba)
     assert np.array_equal(renderer.get_float_image(), sync)
-    f2 = renderer.render_frame(spp_count=1)
+    f2 = renderer.render_frame(spp_count=64)
     f2.cancel()
-    state, payload = f2.poll()
+    while True:
+        state, payload = f2.poll()
+        if state is not FrameInFlightPoll.NotReady:
+            break
     assert state is FrameInFlightPoll.Cancelled and payload is None
+    assert renderer.get_current_spp() == rs.spp  # a cancelled frame does not advance the render
 
 
 def test_validation_errors(renderer):
@@ -310,3 +314,38 @@ def test_c3_grazing_self_hit_regression(torch_cuda, renderer):
     assert segs[770, 269] >= 64
     assert np.array_equal(segs[r0:r1], rsegs[r0:r1])
     assert rel_err(acc[r0:r1], racc[r0:r1]).max() <= REL_TOL_FORWARD
+
+
+@pytest.mark.parametrize("name,res", [("tiny", None), ("C3", (256, 144, 4))])
+def test_megakernel_equals_wavefront(torch_cuda, renderer, name, res):
+    """Both GPU strategies compute every path with the same device functions: bit-identical."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config(name)
+    if res:
+        rs.width, rs.height, rs.spp = res
+    a = gpu_render(torch_cuda, renderer, sc, cam, rs, megakernel=False)
+    b = gpu_render(torch_cuda, renderer, sc, cam, rs, megakernel=True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    for k in ("paths", "segments", "esvo_steps", "sphere_tests", "shade_events"):
+        assert a[2][k] == b[2][k], k
+
+
+def test_wavefront_small_pool_many_chunks(torch_cuda, renderer):
+    """Pool much smaller than the work (path regeneration) and ragged tiles."""
+    import os
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    sc, cam, rs = S.make_config("tiny")
+    rs.width, rs.height, rs.spp = 37, 19, 6
+    ref = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    os.environ["OCTPT_POOL"] = "100"
+    os.environ["OCTPT_REFILL"] = "1"
+    try:
+        small = HipRenderer(0)
+        out = gpu_render(torch_cuda, small, sc, cam, rs)
+        small.close()
+    finally:
+        del os.environ["OCTPT_POOL"], os.environ["OCTPT_REFILL"]
+    assert np.array_equal(ref[0], out[0]) and np.array_equal(ref[1], out[1])
