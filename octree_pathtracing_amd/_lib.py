@@ -162,7 +162,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     if _lib is not None and path is None:
         return _lib
     # OCTPT_LIB: developer override to A/B differently built kernels (same ABI)
-    p = Path(path) if path else Path(os.environ.get("OCTPT_LIB", LIB_PATH))
+    p = Path(path) if path else Path(os.environ.get("OCTPT_LIB") or LIB_PATH)
     try:  # share torch's HIP runtime (same soname libamdhip64.so.7) when torch is present
         import torch  # noqa: F401
     except ImportError:  # pragma: no cover

@@ -27,7 +27,8 @@ namespace {
 constexpr uint32_t kCounterRing = 256;
 constexpr uint64_t kMaxChunkPaths = 128ull << 20;  // colour buffer: 2 GiB of float4 per chunk
 constexpr uint32_t kDefaultPool = 4u << 20;          // path slots in flight
-constexpr uint32_t kDefaultRefill = 32;              // extend: idle lanes before a wave refills
+constexpr uint32_t kDefaultRefill = 24;              // extend: idle lanes before a wave refills
+constexpr uint32_t kDefaultLeafBatch = 0;            // extend: parked lanes before a wave tests leaves (0: inline)
 
 uint32_t env_u32(const char *name, uint32_t dflt) {
     const char *v = std::getenv(name);
@@ -77,9 +78,9 @@ struct octpt_ctx {
     size_t pool = 0, color_cap = 0;
     std::vector<void *> wave_allocs;
     void *color_alloc = nullptr;
-    uint32_t *h_count = nullptr;  // pinned, 2 entries
+    uint32_t *h_count = nullptr;  // pinned: the segment counters of each queue, 2 x kCountSpan words
     hipEvent_t count_ev[2] = {nullptr, nullptr};
-    uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
+    uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill, leaf_batch = kDefaultLeafBatch;
     // one asynchronous frame may be in flight; device-touching calls join it first
     octpt_frame *inflight = nullptr;
 };
@@ -343,9 +344,16 @@ hipError_t wave_alloc(octpt_ctx *ctx, size_t n, T **out) {
     return hipSuccess;
 }
 
+// words from ctr_count(q, 0) through ctr_count(q, kSegs - 1)
+constexpr uint32_t kCountSpan = (kSegs - 1u) * kCtrStride + 1u;
+
+// queue segment capacity: seed wave w fills segment w % kSegs, so ceil(ceil(pool / 64) / kSegs) waves
+size_t seg_cap_for(size_t pool) { return ((pool + 63) / 64 + kSegs - 1) / kSegs * 64; }
+
 octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
     if (!ctx->h_count) {
-        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), 2 * sizeof(uint32_t), hipHostMallocDefault));
+        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), 2 * kCountSpan * sizeof(uint32_t),
+                                   hipHostMallocDefault));
         for (auto &ev : ctx->count_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
     if (pool > ctx->pool) {
@@ -354,15 +362,17 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
         ctx->wave_allocs.clear();
         ctx->pool = 0;
         WaveBuffers &B = ctx->wb;
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray0[0]));
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray0[1]));
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray1[0]));
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.ray1[1]));
+        B.seg_cap = (uint32_t)seg_cap_for(pool);
+        const size_t qlen = (size_t)kSegs * B.seg_cap;  // queue positions
+        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray0[0]));
+        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray0[1]));
+        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray1[0]));
+        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray1[1]));
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pa));
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pb));
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pc));
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.hit));
-        HIP_TRY(ctx, wave_alloc(ctx, 1, &B.ctrl));
+        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.hit));
+        HIP_TRY(ctx, wave_alloc(ctx, kCtrlWords, &B.ctrl));
         ctx->pool = pool;
     }
     if (color_items > ctx->color_cap) {
@@ -403,27 +413,32 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     int &bpc = ctx->extend_bpc_cache[ctx->S.depth];
     if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S.depth);
     const int grid_extend = ctx->num_cu * bpc;
-    const int grid_shade = ctx->num_cu * 4;
+    // shade maps waves to queue segments: a multiple of kSegs waves (kSegs / 4 blocks)
+    const int seg_blocks = (int)(kSegs * 64u / kBlock);
+    const int grid_shade = (ctx->num_cu * 4 + seg_blocks - 1) / seg_blocks * seg_blocks;
     const WaveBuffers &B = ctx->wb;
     for (uint32_t c0 = 0; c0 < R.spp_count; c0 += chunk_spp) {
         DevRender Rc = R;
         Rc.spp_start = R.spp_start + c0;
         Rc.spp_count = std::min(chunk_spp, R.spp_count - c0);
         const uint32_t chunk_items = (uint32_t)((uint64_t)Rc.spp_count * n_px);
-        HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, sizeof(WaveCtrl), s));
+        HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, kCtrlWords * sizeof(uint32_t), s));
         const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
         HIP_TRY(ctx, launch_wf_seed(ctx->C, Rc, B, n_seed, chunk_items, ctx->d_stats, s));
         for (uint32_t it = 0;; ++it) {
             if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
             const uint32_t q = it & 1u;
-            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, grid_extend, ctx->d_stats, s));
+            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, ctx->leaf_batch, grid_extend, ctx->d_stats, s));
             HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, grid_shade, ctx->d_stats, s));
-            HIP_TRY(ctx, hipMemcpyAsync(&ctx->h_count[q], &B.ctrl->count[q ^ 1u], sizeof(uint32_t),
-                                        hipMemcpyDeviceToHost, s));
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_count + q * kCountSpan, B.ctrl + ctr_count(q ^ 1u, 0),
+                                        kCountSpan * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             HIP_TRY(ctx, hipEventRecord(ctx->count_ev[q], s));
             if (it >= 1) {
                 HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[q ^ 1u]));
-                if (ctx->h_count[q ^ 1u] == 0u) break;  // iteration `it` had nothing to do
+                const uint32_t *h = ctx->h_count + (q ^ 1u) * kCountSpan;
+                uint64_t queued = 0;
+                for (uint32_t k = 0; k < kSegs; ++k) queued += h[k * kCtrStride];
+                if (queued == 0u) break;  // iteration `it` had nothing to do
             }
         }
         HIP_TRY(ctx, launch_wf_resolve(Rc, B, Rc.spp_count, d_accum, d_seg, s));
@@ -553,11 +568,12 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->num_cu = prop.multiProcessorCount;
     ctx->pool_cap = env_u32("OCTPT_POOL", kDefaultPool);
     ctx->refill = std::min<uint32_t>(env_u32("OCTPT_REFILL", kDefaultRefill), 64u);
+    ctx->leaf_batch = std::min<uint32_t>(env_u32("OCTPT_LEAF_BATCH", kDefaultLeafBatch), 64u);
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);
-    if (hipMalloc(&ctx->d_stats, kStatCount * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_OOM);
-    if (hipMemset(ctx->d_stats, 0, kStatCount * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    if (hipMalloc(&ctx->d_stats, kStatWords * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_OOM);
+    if (hipMemset(ctx->d_stats, 0, kStatWords * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     float lf[256];
     uint8_t lb[256];
     make_luts(lf, lb);
@@ -965,8 +981,11 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
         (void)hipEventDestroy(e.stop);
     }
     ctx->pending.clear();
-    unsigned long long v[kStatCount];
-    HIP_TRY(ctx, hipMemcpy(v, ctx->d_stats, sizeof v, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> rows(kStatWords);
+    HIP_TRY(ctx, hipMemcpy(rows.data(), ctx->d_stats, kStatWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long v[kStatCount] = {0};
+    for (uint32_t r = 0; r < kSegs; ++r)
+        for (uint32_t i = 0; i < kStatCount; ++i) v[i] += rows[r * kStatRow + i];
     out->paths = v[kStatPaths];
     out->segments = v[kStatSegments];
     out->esvo_steps = v[kStatSteps];
@@ -985,7 +1004,7 @@ octpt_status octpt_reset_stats(octpt_ctx *ctx) {
     octpt_stats tmp;
     octpt_status st = octpt_get_stats(ctx, &tmp);  // drains pending events
     if (st != OCTPT_OK) return st;
-    HIP_TRY(ctx, hipMemset(ctx->d_stats, 0, kStatCount * sizeof(unsigned long long)));
+    HIP_TRY(ctx, hipMemset(ctx->d_stats, 0, kStatWords * sizeof(unsigned long long)));
     ctx->kernel_ms = 0.0;
     ctx->launches = 0;
     return OCTPT_OK;

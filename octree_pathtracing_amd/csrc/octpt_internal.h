@@ -85,13 +85,20 @@ struct DevRender {
     float dim;               // max(W, H)
 };
 
-// wavefront path tracer state
-struct WaveCtrl {
-    uint32_t count[2];   // rays queued in queue[q]
-    uint32_t head[2];    // extend's read cursor into queue[q]
-    uint32_t next_item;  // next chunk work item (pixel x sample) to start
-    uint32_t pad[3];
-};
+// wavefront path tracer state.
+// A single device-scope counter sustains only ~88 M atomicAdd/s on MI355X (tools/atomic_bench.hip),
+// so every queue and work counter is split into kSegs shards, each on its own 256-B line:
+//   ray queue q = kSegs segments of seg_cap positions; segment k holds count(q,k) rays;
+//   extend claims from head(q,k); shade appends a ray to the segment it came from (one input ray
+//   yields at most one output ray, so a segment never overflows); chunk items are split into
+//   kSegs contiguous shards claimed through item(k), stolen from other shards once a wave's own
+//   shard is exhausted.
+constexpr uint32_t kSegs = 64;
+constexpr uint32_t kCtrStride = 64;  // uint32 words between counters (256 B)
+constexpr uint32_t kCtrlWords = 5u * kSegs * kCtrStride;
+__host__ __device__ constexpr uint32_t ctr_count(uint32_t q, uint32_t k) { return (q * kSegs + k) * kCtrStride; }
+__host__ __device__ constexpr uint32_t ctr_head(uint32_t q, uint32_t k) { return ((2u + q) * kSegs + k) * kCtrStride; }
+__host__ __device__ constexpr uint32_t ctr_item(uint32_t k) { return (4u * kSegs + k) * kCtrStride; }
 
 struct WaveBuffers {
     float4 *ray0[2];  // per queue position: (o.xyz, last_prim)
@@ -101,7 +108,8 @@ struct WaveBuffers {
     uint2 *pc;      // (cur_mat, depth | specular << 8 | path_segs << 16)
     uint4 *hit;     // per queue position: (prim, t, inside | axis << 1 | neg << 3, -)
     float4 *color;  // per chunk item: (L.xyz, path segments)
-    WaveCtrl *ctrl;
+    uint32_t *ctrl;    // kCtrlWords sharded counters (see above)
+    uint32_t seg_cap;  // positions per queue segment (multiple of 64)
 };
 
 // per-launch statistics, accumulated with one atomic per wave
@@ -115,6 +123,9 @@ enum StatIndex {
     kStatTexels,
     kStatCount
 };
+// statistics rows: kSegs rows of kStatRow counters (256 B each), row = blockIdx % kSegs; the host sums
+constexpr uint32_t kStatRow = 32;
+constexpr uint32_t kStatWords = kSegs * kStatRow;
 
 // kernel launchers (octpt_kernels.hip)
 hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
@@ -122,8 +133,8 @@ hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender 
                          hipStream_t stream);
 hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t n_seed,
                           uint32_t chunk_items, unsigned long long *stats, hipStream_t stream);
-hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
-                            unsigned long long *stats, hipStream_t stream);
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill,
+                            uint32_t leaf_batch, int grid, unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
                            uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,

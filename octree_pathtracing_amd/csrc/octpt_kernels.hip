@@ -55,6 +55,13 @@ __device__ __forceinline__ float fmn(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float fmx(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float vmin3(v3 a) { return fmn(fmn(a.x, a.y), a.z); }
 __device__ __forceinline__ float vmax3(v3 a) { return fmx(fmx(a.x, a.y), a.z); }
+// ESVO t-values: t_coef is finite and non-zero, pos in [1, 2), so every t is finite and an exact
+// zero difference rounds to +0 -- no NaN and no -0 reach these, and IEEE minNum/maxNum (one
+// v_min3/v_max3) agree bit-for-bit with the a < b ? a : b form the oracle uses.
+__device__ __forceinline__ float tmn(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ float tmx(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ float tmin3(v3 a) { return tmn(tmn(a.x, a.y), a.z); }
+__device__ __forceinline__ float tmax3(v3 a) { return tmx(tmx(a.x, a.y), a.z); }
 __device__ __forceinline__ float signum_(float f) { return (__float_as_uint(f) >> 31) ? -1.0f : 1.0f; }
 
 // ---------------------------------------------------------------------------
@@ -191,6 +198,7 @@ struct Esvo {
     v3 t_coef, t_bias, pos;
     float t_min, t_max, h, scale_exp2;
     uint32_t parent, pmask, idx, mirror, scale, iter;
+    bool resume;  // re-entering a step whose deferred leaf test missed: go straight to advance
 };
 
 struct Counters {
@@ -253,10 +261,12 @@ __device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool s
 
 __device__ __forceinline__ float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6f : 1.0f / d; }
 
-// AABB::intersects_new (aabb.rs:172-191) [C3]
-__device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const TraceRay &r, bool self_prim, PrimHit &h) {
-    // Ray::set_direction's clamped 1/d (mod.rs:91-112), derived from the direction [C12]
-    const v3 inv = V(inv_clamped(r.d.x), inv_clamped(r.d.y), inv_clamped(r.d.z));
+// Ray::set_direction's clamped 1/d (mod.rs:91-112), derived from the direction [C12]
+__device__ __forceinline__ v3 ray_inv_dir(v3 d) { return V(inv_clamped(d.x), inv_clamped(d.y), inv_clamped(d.z)); }
+
+// AABB::intersects_new (aabb.rs:172-191) [C3]; inv = ray_inv_dir(r.d)
+__device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const TraceRay &r, v3 inv, bool self_prim,
+                                            PrimHit &h) {
     const v3 tb = vmul(vsub(V(bmin.x, bmin.y, bmin.z), r.o), inv);
     const v3 tt = vmul(vsub(V(bmax.x, bmax.y, bmax.z), r.o), inv);
     const v3 mins = V(fmn(tb.x, tt.x), fmn(tb.y, tt.y), fmn(tb.z, tt.z));
@@ -400,8 +410,8 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (rd.x > 0.0f) { E.mirror |= 1u; E.t_bias.x = 3.0f * E.t_coef.x - E.t_bias.x; }
     if (rd.y > 0.0f) { E.mirror |= 2u; E.t_bias.y = 3.0f * E.t_coef.y - E.t_bias.y; }
     if (rd.z > 0.0f) { E.mirror |= 4u; E.t_bias.z = 3.0f * E.t_coef.z - E.t_bias.z; }
-    E.t_min = fmx(vmax3(vsub(vscale(E.t_coef, 2.0f), E.t_bias)), 0.0f);
-    E.t_max = vmin3(vsub(E.t_coef, E.t_bias));
+    E.t_min = tmx(tmax3(vsub(vscale(E.t_coef, 2.0f), E.t_bias)), 0.0f);
+    E.t_max = tmin3(vsub(E.t_coef, E.t_bias));
     E.h = E.t_max;
     E.idx = 0u;
     E.pos = V(1.0f, 1.0f, 1.0f);
@@ -410,16 +420,19 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (upper.y > E.t_min) { E.idx ^= 2u; E.pos.y = 1.5f; }
     if (upper.z > E.t_min) { E.idx ^= 4u; E.pos.z = 1.5f; }
     E.iter = 0u;
+    E.resume = false;
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
-// common single-primitive leaf (one dependent load fewer).
-__device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_exit_w, float cell_w,
+// common single-primitive leaf (one dependent load fewer).  t_accept = t_exit_w + CELL_TOL * cell_w.
+__device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt) {
-    const float t_accept = t_exit_w + CELL_TOL * cell_w;
     bool found = false;
+    // three correctly-rounded divides: only scenes holding cuboids pay for them (uniform branch)
+    v3 inv = V(0.0f, 0.0f, 0.0f);
+    if (S.has_cuboids) inv = ray_inv_dir(r.d);
     for (uint32_t k = 0; k < lr.y; ++k) {
         const uint32_t prim = lr.y == 1u ? lr.x : S.leaf_prims[lr.x + k];
         const bool self_prim = prim == r.last_prim;
@@ -431,7 +444,7 @@ __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr,
         } else {
             cnt.cub++;
             const uint32_t ci = prim & ~kPrimCuboidBit;
-            ok = cuboid_test(S.cub_min[ci], S.cub_max[ci], r, self_prim, h);
+            ok = cuboid_test(S.cub_min[ci], S.cub_max[ci], r, inv, self_prim, h);
         }
         if (ok && h.t <= t_accept && (!found || h.t < best.t)) {
             best = h;
@@ -442,31 +455,48 @@ __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr,
     return found;
 }
 
-// one ESVO iteration; on kStepHit (prim, h) hold the accepted primitive hit
+enum : int { kStepLeaf = 3 };
+
+// one ESVO iteration; on kStepHit (prim, h) hold the accepted primitive hit.  kDefer: a leaf is
+// not tested here -- the step returns kStepLeaf with (leaf, t_accept) and E.resume set; the caller
+// tests the leaf later (wave-batched) and, on a miss, calls esvo_step again, which then performs
+// the same iteration's advance without counting the iteration twice (octree_traversal.rs:142-260).
+template <bool kDefer>
 __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const Stack &stk, Counters &cnt,
-                                uint32_t &prim, PrimHit &h) {
+                                uint32_t &prim, PrimHit &h, uint2 &leaf, float &t_accept) {
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
-    if (E.iter >= OCTREE_MAX_STEPS) return kStepMiss;
-    if (max_dst >= 0.0f && E.t_min > max_dst) return kStepMiss;
-    E.iter++;
-    cnt.steps++;
+    const bool resume = kDefer && E.resume;
+    if (!resume) {
+        // on a resumed step these were checked before the deferred leaf: iter may now equal
+        // OCTREE_MAX_STEPS, and exiting here is the same miss the reference reaches after its advance
+        if (E.iter >= OCTREE_MAX_STEPS) return kStepMiss;
+        if (max_dst >= 0.0f && E.t_min > max_dst) return kStepMiss;
+        E.iter++;  // callers add E.iter to cnt.steps when the ray finishes
+    }
+    if (kDefer) E.resume = false;
     const v3 t_corner = vsub(vmul(E.pos, E.t_coef), E.t_bias);
-    const float tc_max = vmin3(t_corner);
+    const float tc_max = tmin3(t_corner);
     const uint32_t cidx = E.idx ^ E.mirror;
     const bool present = (E.pmask >> cidx) & 1u;
     const bool is_leaf = (E.pmask >> (cidx + 8u)) & 1u;
     // :142-244.  Leaf (t_min >= 0) and descend (t_min <= min(t_max, tc_max)) lanes share one slot
     // load instruction: on CDNA4 a scattered load costs the vector-memory pipe per instruction.
     const bool live = present && E.t_min <= E.t_max;
-    const float tv_max = fmn(E.t_max, tc_max);
-    const bool take_leaf = live && is_leaf && E.t_min >= 0.0f;
+    const float tv_max = tmn(E.t_max, tc_max);
+    const bool take_leaf = live && is_leaf && E.t_min >= 0.0f && !resume;
     const bool descend = live && !is_leaf && E.t_min <= tv_max;
     uint2 slot = make_uint2(0u, 0u);
     if (take_leaf || descend) slot = S.node_child[8u * E.parent + cidx];
     if (take_leaf) {
         // x / 2^-depth == x * 2^depth exactly (the oracle divides)
         const float cell_w = E.scale_exp2 * S.inv_octree_scale;
-        if (leaf_test(S, ray, slot, tc_max * S.inv_octree_scale, cell_w, prim, h, cnt)) return kStepHit;
+        t_accept = tc_max * S.inv_octree_scale + CELL_TOL * cell_w;
+        if (kDefer) {
+            leaf = slot;
+            E.resume = true;
+            return kStepLeaf;
+        }
+        if (leaf_test(S, ray, slot, t_accept, prim, h, cnt)) return kStepHit;
     } else if (descend) {
         const float half = E.scale_exp2 * 0.5f;
         const v3 t_center = vadd(vscale(E.t_coef, half), t_corner);
@@ -811,7 +841,7 @@ __device__ inline void flush_counters(const Counters &cnt, unsigned long long *s
 #pragma unroll
     for (int i = 0; i < kStatCount; ++i) {
         const unsigned long long s = wave_sum(vals[i]);
-        if ((threadIdx.x & 63u) == 0u && s) atomicAdd(&stats[i], s);
+        if ((threadIdx.x & 63u) == 0u && s) atomicAdd(&stats[(blockIdx.x % kSegs) * kStatRow + i], s);
     }
 }
 
@@ -894,9 +924,12 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             }
             first = false;
             if (state == ST_TRAV) {
-                const int rs = esvo_step(S, tr, E, stk, cnt, hprim, hh);
+                uint2 lf;
+                float ta;
+                const int rs = esvo_step<false>(S, tr, E, stk, cnt, hprim, hh, lf, ta);
                 if (rs == kStepHit) state = ST_HIT;
                 else if (rs == kStepMiss) state = ST_MISS;
+                if (rs != kStepContinue) cnt.steps += E.iter;
             }
         }
         if (state == ST_HIT || state == ST_MISS || state == ST_FINISH) {
@@ -979,34 +1012,67 @@ __device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const W
     return true;
 }
 
-// lanes with `want` start the next chunk items in their slots; items whose pixel lies outside
-// the image are consumed (zero colour) and the lane draws again, so a slot only goes idle
-// once the chunk has no items left.  Every lane of the wave must call this.
+static_assert(kSegs == 64, "segment scans give one wave lane per segment");
+
+__device__ __forceinline__ uint32_t relaxed_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// chunk item shard k = [shard_lo(k), shard_lo(k + 1))
+__device__ __forceinline__ uint32_t shard_lo(uint32_t k, uint32_t n) {
+    return (uint32_t)(((uint64_t)k * n) / kSegs);
+}
+// first set bit of m at or after bit `from`, cyclically; m != 0
+__device__ __forceinline__ uint32_t first_from(uint64_t m, uint32_t from) {
+    const uint64_t r = from ? ((m >> from) | (m << (64u - from))) : m;
+    return (from + (uint32_t)__ffsll((unsigned long long)r) - 1u) & 63u;
+}
+
+// Item claims of one wave: the shard it is drawing from and whether any shard has items left
+// (both wave-uniform).
+struct ItemCursor {
+    uint32_t k;
+    bool left;
+};
+
+// lanes with `want` start the next chunk items in their slots.  The wave draws from shard
+// cur.k; when that runs dry, one relaxed load per lane (lane j = shard j) finds the next shard
+// with items left.  Items whose pixel lies outside the image are consumed (zero colour) and the
+// lane draws again, so a slot only goes idle once every shard is exhausted.  Every lane of the
+// wave must call this.
 __device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t slot, bool want,
-                             uint32_t chunk_items, PathState &ps, Counters &cnt) {
+                             uint32_t chunk_items, ItemCursor &cur, PathState &ps, Counters &cnt) {
     bool need = want, ok = false;
-    while (__ballot(need) != 0ull) {
-        const uint32_t ni = wave_ticket(&B.ctrl->next_item, need);
+    while (cur.left && __ballot(need) != 0ull) {
+        const uint32_t lo = shard_lo(cur.k, chunk_items), n = shard_lo(cur.k + 1u, chunk_items) - lo;
+        const uint32_t t = wave_ticket(B.ctrl + ctr_item(cur.k), need);
+        bool dry = false;
         if (need) {
-            if (ni >= chunk_items) {
-                need = false;
-            } else if (seed_item(C, R, B, slot, ni, ps, cnt)) {
-                ok = true;
-                need = false;
-            }
+            if (t >= n) dry = true;
+            else if (seed_item(C, R, B, slot, lo + t, ps, cnt)) { ok = true; need = false; }
+        }
+        if (__ballot(dry) != 0ull) {
+            const uint32_t j = threadIdx.x & 63u;
+            const bool has = relaxed_load(B.ctrl + ctr_item(j)) < shard_lo(j + 1u, chunk_items) - shard_lo(j, chunk_items);
+            const uint64_t m = __ballot(has);
+            cur.left = m != 0ull;
+            if (cur.left) cur.k = first_from(m, cur.k);
         }
     }
     return ok;
 }
 
+// seed: slot i starts a path; wave w appends to queue 0 segment w % kSegs, which holds at most
+// seg_cap rays (seg_cap = ceil(ceil(pool / 64) / kSegs) * 64)
 __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender R, WaveBuffers B, uint32_t n_seed,
                                                          uint32_t chunk_items, unsigned long long *__restrict__ stats) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t seg = (i >> 6) % kSegs;
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     PathState ps;
-    const bool ok = regen(C, R, B, i, i < n_seed, chunk_items, ps, cnt);
-    const uint32_t pos = wave_ticket(&B.ctrl->count[0], ok);
-    if (ok) store_ray(B, 0u, pos, i, ps);
+    ItemCursor cur = {seg, true};
+    const bool ok = regen(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
+    const uint32_t t = wave_ticket(B.ctrl + ctr_count(0u, seg), ok);
+    if (ok) store_ray(B, 0u, seg * B.seg_cap + t, i, ps);
     flush_counters(cnt, stats);
 }
 
@@ -1016,51 +1082,86 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #ifndef OCTPT_EXTEND_WAVES
 #define OCTPT_EXTEND_WAVES 1
 #endif
+template <bool kDefer>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
-                                                           unsigned long long *__restrict__ stats) {
+                                                           uint32_t leaf_batch, unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
     const Stack stk = stack_of(lds_stack, S.depth);
-    const uint32_t count = B.ctrl->count[q];
     const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the other queue is refilled by this iteration's shade
-        B.ctrl->count[q ^ 1u] = 0u;
-        B.ctrl->head[q ^ 1u] = 0u;
+    if (blockIdx.x == 0 && threadIdx.x < kSegs) {  // the other queue is refilled by this iteration's shade
+        B.ctrl[ctr_count(q ^ 1u, threadIdx.x)] = 0u;
+        B.ctrl[ctr_head(q ^ 1u, threadIdx.x)] = 0u;
     }
+    // the wave starts on its home segment (seg, seg_n rays: wave-uniform)
+    uint32_t seg = __builtin_amdgcn_readfirstlane(((blockIdx.x * kBlock + threadIdx.x) >> 6) % kSegs);
+    uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
+    bool rays_left = true;  // wave-uniform: some segment may still hold unclaimed rays
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    bool active = false, done = false;
+    bool active = false, pend = false;
     uint32_t pos = 0u;
     TraceRay tr;
     Esvo E;
+    uint2 leaf = make_uint2(0u, 0u);
+    float t_accept = 0.0f;
     for (;;) {
-        const bool idle = !active && !done;
+        const bool idle = !active;
         const uint64_t im = __ballot(idle);
-        if (im != 0ull && ((uint32_t)__popcll(im) >= refill || __ballot(active) == 0ull)) {
-            const uint32_t my = wave_ticket(&B.ctrl->head[q], idle);
+        if (rays_left && im != 0ull && ((uint32_t)__popcll(im) >= refill || ~im == 0ull)) {
+            const uint32_t my = wave_ticket(B.ctrl + ctr_head(q, seg), idle);
+            bool dry = false;
             if (idle) {
-                if (my < count) {
-                    pos = my;
-                    const float4 r0 = ray0[my], r1 = ray1[my];
+                if (my < seg_n) {
+                    pos = seg * B.seg_cap + my;
+                    const float4 r0 = ray0[pos], r1 = ray1[pos];
                     tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk);
                     cnt.segs++;
                     active = true;
                 } else {
-                    done = true;
+                    dry = true;
+                }
+            }
+            if (__ballot(dry) != 0ull) {  // segment drained: lane j checks segment j, the wave moves on
+                const uint32_t j = threadIdx.x & 63u;
+                const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, j)) < B.ctrl[ctr_count(q, j)]);
+                rays_left = m != 0ull;
+                if (rays_left) {
+                    seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
+                    seg_n = B.ctrl[ctr_count(q, seg)];
                 }
             }
         }
-        if (__ballot(active) == 0ull) break;
-        if (active) {
+        const uint64_t am = __ballot(active);
+        if (am == 0ull && !rays_left) break;  // (am == 0 with rays left: the next pass refills)
+        // deferred leaf tests [kStepLeaf]: run once leaf_batch lanes wait, or every active lane does
+        const uint64_t pm = kDefer ? __ballot(pend) : 0ull;
+        if (pm != 0ull && ((uint32_t)__popcll(pm) >= leaf_batch || pm == am)) {
+            if (pend) {
+                pend = false;
+                uint32_t prim = kPrimNone;
+                PrimHit h;
+                if (leaf_test(S, tr, leaf, t_accept, prim, h, cnt)) {
+                    B.hit[pos] = make_uint4(prim, __float_as_uint(h.t),
+                                            h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u), 0u);
+                    cnt.steps += E.iter;
+                    active = false;
+                }
+            }
+        }
+        if (active && !pend) {
             uint32_t prim = kPrimNone;
             PrimHit h;
-            const int rs = esvo_step(S, tr, E, stk, cnt, prim, h);
-            if (rs != kStepContinue) {
+            const int rs = esvo_step<kDefer>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
+            if (rs == kStepLeaf) {
+                pend = true;
+            } else if (rs != kStepContinue) {
                 uint4 rec = make_uint4(kPrimNone, 0u, 0u, 0u);
                 if (rs == kStepHit)
                     rec = make_uint4(prim, __float_as_uint(h.t),
                                      h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u), 0u);
                 B.hit[pos] = rec;
+                cnt.steps += E.iter;
                 active = false;
             }
         }
@@ -1072,14 +1173,19 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
 __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items,
                                                           unsigned long long *__restrict__ stats) {
-    const uint32_t count = B.ctrl->count[q];
+    // wave w shades segment w % kSegs of queue q (grid: a multiple of kSegs waves) and appends
+    // the continuing / regenerated rays to the same segment of queue q ^ 1
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
+    const uint32_t seg = wave % kSegs;
+    const uint32_t seg_waves = ((gridDim.x * kBlock) >> 6) / kSegs;
+    const uint32_t count = B.ctrl[ctr_count(q, seg)];
+    const uint32_t seg0 = seg * B.seg_cap;
+    ItemCursor cur = {seg, true};
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    for (uint32_t base = wave * 64u; base < count; base += n_waves * 64u) {
-        const uint32_t i = base + lane;
-        const bool valid = i < count;
+    for (uint32_t base = (wave / kSegs) * 64u; base < count; base += seg_waves * 64u) {
+        const uint32_t i = seg0 + base + lane;
+        const bool valid = base + lane < count;
         uint32_t slot = 0u, item = 0u;
         bool append = false, finished = false;
         PathState ps;
@@ -1109,9 +1215,9 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, DevCamera 
             }
         }
         // regenerate: finished lanes take the next chunk items (path regeneration)
-        if (regen(C, R, B, slot, finished, chunk_items, ps, cnt)) append = true;
-        const uint32_t pos = wave_ticket(&B.ctrl->count[q ^ 1u], append);
-        if (append) store_ray(B, q ^ 1u, pos, slot, ps);
+        if (regen(C, R, B, slot, finished, chunk_items, cur, ps, cnt)) append = true;
+        const uint32_t t = wave_ticket(B.ctrl + ctr_count(q ^ 1u, seg), append);
+        if (append) store_ray(B, q ^ 1u, seg0 + t, slot, ps);
     }
     flush_counters(cnt, stats);
 }
@@ -1161,7 +1267,9 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
     PrimHit h;
     int rs;
     do {
-        rs = esvo_step(S, tr, E, stk, cnt, prim, h);
+        uint2 lf;
+        float ta;
+        rs = esvo_step<false>(S, tr, E, stk, cnt, prim, h, lf, ta);
     } while (rs == kStepContinue);
     if (rs == kStepHit) {
         commit_hit(S, ps, prim, h, cnt);
@@ -1214,10 +1322,13 @@ int render_blocks_per_cu(uint32_t depth) {
 }
 
 int extend_blocks_per_cu(uint32_t depth) {
-    int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void *>(wf_extend_kernel), kBlock,
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, reinterpret_cast<const void *>(wf_extend_kernel<true>), kBlock,
+                                                     render_lds_bytes(depth)) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void *>(wf_extend_kernel<false>), kBlock,
                                                      render_lds_bytes(depth)) != hipSuccess)
         return 1;
+    const int blocks = a < b ? a : b;
     return blocks > 0 ? blocks : 1;
 }
 
@@ -1235,10 +1346,15 @@ hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuff
     return hipGetLastError();
 }
 
-hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
-                            unsigned long long *stats, hipStream_t stream) {
-    hipLaunchKernelGGL(wf_extend_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, B, q, refill,
-                       stats);
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill,
+                            uint32_t leaf_batch, int grid, unsigned long long *stats, hipStream_t stream) {
+    // leaf_batch 0: test leaves inside the step (no deferral)
+    if (leaf_batch == 0u)
+        hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, B, q,
+                           refill, leaf_batch, stats);
+    else
+        hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, B, q,
+                           refill, leaf_batch, stats);
     return hipGetLastError();
 }
 
