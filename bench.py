@@ -9,9 +9,13 @@ renders its tiles into a compact buffer and the tiles are gathered to rank 0 ove
 (all_gather_into_tensor) and scattered into the frame by octpt_unshard_device.
 
 value = total ray segments (closest-hit queries, all ranks) / wall time of the K timed steps
-(max over ranks).  roofline.achieved = algorithmic bytes per render launch /
-the launch's average HIP-event duration.  cpu_baseline = the oracle (oracle/cpu_ref.c, a
-C port of the reference's CPU TileRenderer) timed on this host on a bounded sample.
+(max over ranks).  roofline: the dominant kernel is wf_extend_kernel (octree traversal +
+primitive tests, ~90 % of GPU time); achieved = its algorithmic bytes per launch
+/ its average launch duration, both measured live: every extend / shade launch of the timed
+steps is bracketed by HIP events on the render stream (OCTPT_RENDER_KERNEL_TIMING).  traffic =
+the L2-to-fabric bytes per extend launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+committed in profiles/pmc_<config>.json.  cpu_baseline = the oracle (oracle/cpu_ref.c, a C port
+of the reference's CPU TileRenderer) timed on this host on a bounded sample.
 """
 from __future__ import annotations
 
@@ -31,12 +35,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 METRIC = "Mrays/sec at 1920×1080×256spp; achieved HBM GB/s vs roofline at 1/2/4/8 GPUs"
 
 
-def algorithmic_bytes(st: dict) -> float:
-    """8 B per ESVO iteration (child mask + child word), 16+4 B per sphere test
-    (float4 + leaf prim index), 24+4 B per cuboid test, 32 B per shaded hit (GPUMaterial),
-    4 B per texel, 16 B per path (running-mean read-modify-write of the F32Color)."""
-    return (8.0 * st["esvo_steps"] + 20.0 * st["sphere_tests"] + 28.0 * st["cuboid_tests"]
-            + 32.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
+def extend_bytes(st: dict) -> float:
+    """DESIGN.md §8, wf_extend_kernel: 8 B per ESVO iteration (one packed child slot), 16 + 4 B per
+    sphere test (centre/radius float4 + leaf prim index), 32 + 4 B per cuboid test (min/max
+    float4s + index), 48 B per segment (32-B ray record read + 16-B hit record write)."""
+    return (8.0 * st["esvo_steps"] + 20.0 * st["sphere_tests"] + 36.0 * st["cuboid_tests"]
+            + 48.0 * st["segments"])
+
+
+def shade_bytes(st: dict) -> float:
+    """DESIGN.md §8, wf_shade_kernel per segment: ray record 32 + hit 16 + path state 40 read,
+    path state 40 + ray record 32 written; per shaded hit 16 (sphere) + 4 (material id) + 48
+    (material record); 4 B per texel; 16 B per finished path (colour record)."""
+    return (160.0 * st["segments"] + 68.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
 
 
 def load_traffic(config: str):
@@ -44,7 +55,7 @@ def load_traffic(config: str):
     if p.exists():
         try:
             d = json.loads(p.read_text())
-            return d.get("hbm_bytes_per_launch")
+            return d.get("wf_extend_kernel", {}).get("bytes_per_launch")
         except Exception:
             return None
     return None
@@ -111,7 +122,7 @@ def main():
     accum[:, 3] = 1.0
     gbuf = torch.zeros((world * stride, 4), dtype=torch.float32, device=dev) if world > 1 else None
     frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev) if (world > 1 and rank == 0) else None
-    params = r.params(W, H, 0, rs.spp, rank, world, compact=True)
+    params = r.params(W, H, 0, rs.spp, rank, world, compact=True, kernel_timing=True)
 
     def step():
         stream = torch.cuda.current_stream().cuda_stream
@@ -145,10 +156,13 @@ def main():
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         seg = int(s.item())
 
-    launches = max(st["launches"], 1)
-    kernel_s = st["kernel_ms"] / 1e3 / launches
-    bytes_per_launch = algorithmic_bytes(st) / launches
-    achieved = bytes_per_launch / kernel_s / 1e9 if kernel_s > 0 else 0.0
+    n_ext = max(st["extend_launches"], 1)
+    ext_s = st["extend_ms"] / 1e3 / n_ext
+    bytes_per_launch = extend_bytes(st) / n_ext
+    achieved = bytes_per_launch / ext_s / 1e9 if ext_s > 0 else 0.0
+    n_sh = max(st["shade_launches"], 1)
+    sh_s = st["shade_ms"] / 1e3 / n_sh
+    sh_bytes = shade_bytes(st) / n_sh
     traffic = load_traffic(args.config)
     out = {
         "metric": METRIC,
@@ -179,9 +193,14 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "render_kernel",
-            "kernel_ms_avg": round(kernel_s * 1e3, 3),
+            "kernel": "wf_extend_kernel",
+            "launches": st["extend_launches"],
+            "kernel_ms_avg": round(ext_s * 1e3, 4),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "share_of_gpu_time": round(st["extend_ms"] / max(st["extend_ms"] + st["shade_ms"], 1e-9), 3),
+            "shade": {"kernel": "wf_shade_kernel", "launches": st["shade_launches"],
+                      "kernel_ms_avg": round(sh_s * 1e3, 4), "algorithmic_bytes_per_launch": int(sh_bytes),
+                      "achieved": round(sh_bytes / sh_s / 1e9, 1) if sh_s > 0 else 0.0},
         },
         "stats_rank0": {k: v for k, v in st.items() if k != "kernel_ms"},
     }

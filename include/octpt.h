@@ -133,6 +133,7 @@ typedef struct octpt_camera {
  * (tile_renderer.rs:684-734) continuing a running mean that already holds spp_start samples. */
 #define OCTPT_RENDER_SHARD_COMPACT 0x1u /* accum holds only this shard's 8x8 tiles, tile-major */
 #define OCTPT_RENDER_MEGAKERNEL 0x2u    /* single persistent megakernel instead of the wavefront loop (A/B) */
+#define OCTPT_RENDER_KERNEL_TIMING 0x4u /* bracket every extend / shade launch with HIP events (octpt_stats) */
 typedef struct octpt_render_params {
     uint32_t width, height;
     uint32_t spp_start, spp_count;
@@ -146,7 +147,10 @@ typedef struct octpt_render_params {
 typedef struct octpt_stats {
     uint64_t paths, segments, esvo_steps, sphere_tests, cuboid_tests, shade_events, texel_reads;
     uint64_t launches;
-    double kernel_ms; /* HIP-event time of the render kernels since the last reset */
+    double kernel_ms; /* HIP-event time of the render calls since the last reset */
+    /* per-kernel HIP-event time of the wavefront loop, renders flagged OCTPT_RENDER_KERNEL_TIMING only */
+    uint64_t extend_launches, shade_launches;
+    double extend_ms, shade_ms;
 } octpt_stats;
 
 /* --- library / context ------------------------------------------------------ */

@@ -28,6 +28,7 @@ TEXTURE_COLOR = 0
 TEXTURE_IMAGE = 1
 RENDER_SHARD_COMPACT = 0x1
 RENDER_MEGAKERNEL = 0x2
+RENDER_KERNEL_TIMING = 0x4
 PRIM_NONE = 0xFFFFFFFF
 PRIM_CUBOID_BIT = 0x80000000
 
@@ -112,7 +113,9 @@ class RenderParams(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("esvo_steps", C.c_uint64),
                 ("sphere_tests", C.c_uint64), ("cuboid_tests", C.c_uint64), ("shade_events", C.c_uint64),
-                ("texel_reads", C.c_uint64), ("launches", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("texel_reads", C.c_uint64), ("launches", C.c_uint64), ("kernel_ms", C.c_double),
+                ("extend_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("extend_ms", C.c_double),
+                ("shade_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -71,6 +71,12 @@ struct octpt_ctx {
     std::vector<EventPair> pending;
     double kernel_ms = 0.0;
     uint64_t launches = 0;
+    // per-kernel timing (OCTPT_RENDER_KERNEL_TIMING): kind 0 extend, 1 shade
+    bool ktiming = false;
+    std::vector<std::pair<int, EventPair>> kpending;
+    std::vector<EventPair> ev_pool;
+    double kern_ms[2] = {0.0, 0.0};
+    uint64_t kern_n[2] = {0, 0};
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
     int extend_bpc_cache[kMaxDepth + 1] = {0};
     // wavefront pool (grown on demand)
@@ -315,6 +321,7 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     R.shard_index = p->shard_index;
     R.shard_count = p->shard_count;
     R.compact = (p->flags & OCTPT_RENDER_SHARD_COMPACT) ? 1u : 0u;
+    ctx->ktiming = (p->flags & OCTPT_RENDER_KERNEL_TIMING) != 0;
     R.tiles_x = (p->width + kTile - 1) / kTile;
     const uint32_t tiles_y = (p->height + kTile - 1) / kTile;
     R.shard_tiles = tiles_of_shard(R.tiles_x * tiles_y, p->shard_index, p->shard_count);
@@ -387,6 +394,27 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
     return OCTPT_OK;
 }
 
+// begin / end a timed kernel launch of `kind` on stream s (no-op unless ctx->ktiming)
+octpt_status ktimer_begin(octpt_ctx *ctx, hipStream_t s, EventPair &ev) {
+    if (!ctx->ktiming) return OCTPT_OK;
+    if (ctx->ev_pool.empty()) {
+        EventPair e{};
+        HIP_TRY(ctx, hipEventCreate(&e.start));
+        HIP_TRY(ctx, hipEventCreate(&e.stop));
+        ctx->ev_pool.push_back(e);
+    }
+    ev = ctx->ev_pool.back();
+    ctx->ev_pool.pop_back();
+    HIP_TRY(ctx, hipEventRecord(ev.start, s));
+    return OCTPT_OK;
+}
+octpt_status ktimer_end(octpt_ctx *ctx, hipStream_t s, int kind, const EventPair &ev) {
+    if (!ctx->ktiming) return OCTPT_OK;
+    ctx->kpending.emplace_back(kind, ev);
+    HIP_TRY(ctx, hipEventRecord(ev.stop, s));
+    return OCTPT_OK;
+}
+
 // megakernel variant (OCTPT_RENDER_MEGAKERNEL): one persistent launch per call
 octpt_status enqueue_megakernel(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s) {
     uint32_t *counter = ctx->d_counters + (ctx->launch_seq++ % kCounterRing);
@@ -428,8 +456,13 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         for (uint32_t it = 0;; ++it) {
             if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
             const uint32_t q = it & 1u;
+            EventPair ev{};
+            if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
             HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, ctx->leaf_batch, grid_extend, ctx->d_stats, s));
+            if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
+            if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
             HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, grid_shade, ctx->d_stats, s));
+            if ((st = ktimer_end(ctx, s, 1, ev)) != OCTPT_OK) return st;
             HIP_TRY(ctx, hipMemcpyAsync(ctx->h_count + q * kCountSpan, B.ctrl + ctr_count(q ^ 1u, 0),
                                         kCountSpan * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             HIP_TRY(ctx, hipEventRecord(ctx->count_ev[q], s));
@@ -591,6 +624,12 @@ void octpt_destroy(octpt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto &e : ctx->pending) {
+        (void)hipEventSynchronize(e.stop);
+        (void)hipEventDestroy(e.start);
+        (void)hipEventDestroy(e.stop);
+    }
+    for (auto &ke : ctx->kpending) ctx->ev_pool.push_back(ke.second);
+    for (auto &e : ctx->ev_pool) {
         (void)hipEventSynchronize(e.stop);
         (void)hipEventDestroy(e.start);
         (void)hipEventDestroy(e.stop);
@@ -981,6 +1020,15 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
         (void)hipEventDestroy(e.stop);
     }
     ctx->pending.clear();
+    for (auto &ke : ctx->kpending) {
+        HIP_TRY(ctx, hipEventSynchronize(ke.second.stop));
+        float ms = 0.0f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ke.second.start, ke.second.stop));
+        ctx->kern_ms[ke.first] += ms;
+        ctx->kern_n[ke.first]++;
+        ctx->ev_pool.push_back(ke.second);
+    }
+    ctx->kpending.clear();
     std::vector<unsigned long long> rows(kStatWords);
     HIP_TRY(ctx, hipMemcpy(rows.data(), ctx->d_stats, kStatWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     unsigned long long v[kStatCount] = {0};
@@ -995,6 +1043,10 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     out->texel_reads = v[kStatTexels];
     out->launches = ctx->launches;
     out->kernel_ms = ctx->kernel_ms;
+    out->extend_launches = ctx->kern_n[0];
+    out->shade_launches = ctx->kern_n[1];
+    out->extend_ms = ctx->kern_ms[0];
+    out->shade_ms = ctx->kern_ms[1];
     return OCTPT_OK;
 }
 
@@ -1007,6 +1059,8 @@ octpt_status octpt_reset_stats(octpt_ctx *ctx) {
     HIP_TRY(ctx, hipMemset(ctx->d_stats, 0, kStatWords * sizeof(unsigned long long)));
     ctx->kernel_ms = 0.0;
     ctx->launches = 0;
+    ctx->kern_ms[0] = ctx->kern_ms[1] = 0.0;
+    ctx->kern_n[0] = ctx->kern_n[1] = 0;
     return OCTPT_OK;
 }
 

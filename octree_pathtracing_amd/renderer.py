@@ -206,8 +206,9 @@ class HipRenderer:
 
     # ------------------------------------------------------------ direct entry points
     def params(self, W, H, spp_start, spp_count, shard_index=0, shard_count=1, compact=False,
-               megakernel=False) -> "_lib.RenderParams":
-        flags = (_lib.RENDER_SHARD_COMPACT if compact else 0) | (_lib.RENDER_MEGAKERNEL if megakernel else 0)
+               megakernel=False, kernel_timing=False) -> "_lib.RenderParams":
+        flags = ((_lib.RENDER_SHARD_COMPACT if compact else 0) | (_lib.RENDER_MEGAKERNEL if megakernel else 0)
+                 | (_lib.RENDER_KERNEL_TIMING if kernel_timing else 0))
         return _lib.RenderParams(W, H, spp_start, spp_count, self.max_depth, 1, self.seed, shard_index, shard_count,
                                  flags)
 
