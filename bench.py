@@ -105,6 +105,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.distributed import gather_frame
     from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
 
     sc, cam, rs = S.make_config(args.config)
@@ -127,10 +128,9 @@ def main():
     def step():
         stream = torch.cuda.current_stream().cuda_stream
         r.render_device(params, accum.data_ptr(), None, stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gbuf, accum)  # RCCL over xGMI
-            if rank == 0:
-                r.unshard_device(W, H, world, gbuf.data_ptr(), stride, frame.data_ptr(), stream)
+        if world > 1:  # RCCL all_gather_into_tensor over xGMI, then the unshard kernel on rank 0
+            gather_frame(accum, gbuf, W, H, rank, world,
+                         lambda g: r.unshard_device(W, H, world, g.data_ptr(), stride, frame.data_ptr(), stream))
 
     for _ in range(args.warmup):
         step()

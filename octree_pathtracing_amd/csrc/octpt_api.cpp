@@ -27,6 +27,7 @@ namespace {
 constexpr uint32_t kCounterRing = 256;
 constexpr uint64_t kMaxChunkPaths = 128ull << 20;  // colour buffer: 2 GiB of float4 per chunk
 constexpr uint32_t kDefaultPool = 4u << 20;          // path slots in flight
+constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
 constexpr uint32_t kDefaultRefill = 24;              // extend: idle lanes before a wave refills
 constexpr uint32_t kDefaultLeafBatch = 0;            // extend: parked lanes before a wave tests leaves (0: inline)
 
@@ -1072,7 +1073,29 @@ octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const 
     if ((ns && !spheres) || (nc && !cuboids)) return OCTPT_ERR_INVALID_ARG;
     try {
         const int32_t N = 1 << depth;
+        // upper bound of the (cell, primitive) pairs: the clamped bounding-box cells of every
+        // primitive.  Leaf tables index pairs with uint32, and a scene past 2^31 pairs (>= 32 GiB
+        // of pairs) is refused up front rather than discovered by allocating until bad_alloc.
+        uint64_t bound = 0;
+        auto add_box = [&](const float *lo_f, const float *hi_f) {
+            uint64_t cells = 1;
+            for (int a = 0; a < 3; ++a) {
+                const float fl = floorf(lo_f[a]), fh = floorf(hi_f[a]);
+                if (fh < 0.0f || fl > (float)(N - 1) || hi_f[a] < lo_f[a]) return;
+                cells *= (uint64_t)(clamp_cell(fh, N - 1) - clamp_cell(fl, N - 1) + 1);
+            }
+            bound = std::min<uint64_t>(bound + cells, UINT64_MAX / 2);
+        };
+        for (uint32_t i = 0; i < ns; ++i) {
+            const float *c = spheres[i].center, r = spheres[i].radius;
+            if (!(r > 0.0f)) continue;
+            const float lo_f[3] = {c[0] - r, c[1] - r, c[2] - r}, hi_f[3] = {c[0] + r, c[1] + r, c[2] + r};
+            add_box(lo_f, hi_f);
+        }
+        for (uint32_t i = 0; i < nc; ++i) add_box(cuboids[i].min, cuboids[i].max);
+        if (bound > kMaxBuildPairs) return OCTPT_ERR_OOM;
         std::vector<CellPrim> cells;
+        cells.reserve((size_t)std::min<uint64_t>(bound, 1ull << 24));
         for (uint32_t i = 0; i < ns; ++i) {
             const float *c = spheres[i].center;
             const float r = spheres[i].radius;

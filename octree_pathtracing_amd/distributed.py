@@ -1,0 +1,79 @@
+"""Multi-GPU tile sharding of the render: one process per GPU.
+
+The frame's 8x8 pixel tiles are dealt round-robin, tile t -> rank t % N; rank k renders its tiles
+into a compact buffer (OCTPT_RENDER_SHARD_COMPACT: tile-major, 64 pixels per tile, row-major inside
+the tile -- the kernels' item_pixel mapping, octpt_kernels.hip) of `stride` pixels (the largest
+shard), the compact buffers are all-gathered (RCCL over xGMI on the GPUs, gloo in the CPU tests)
+and rank 0 scatters them back into the frame (octpt_unshard_device on the GPU, unshard_host here).
+Per-pixel RNG streams are keyed by pixel and sample, never by rank, so a sharded render equals the
+unsharded one bit for bit.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+TILE = 8
+
+
+def tiles_xy(W: int, H: int):
+    return (W + TILE - 1) // TILE, (H + TILE - 1) // TILE
+
+
+def shard_tile_count(W: int, H: int, k: int, N: int) -> int:
+    tx, ty = tiles_xy(W, H)
+    tiles = tx * ty
+    return len(range(k, tiles, N))
+
+
+def shard_stride(W: int, H: int, N: int) -> int:
+    """Pixels per compact shard buffer: the largest shard (shard 0)."""
+    return shard_tile_count(W, H, 0, N) * TILE * TILE
+
+
+def shard_layout(W: int, H: int, k: int, N: int) -> np.ndarray:
+    """Frame pixel index (y * W + x) of every compact slot of shard k; -1 where the tile overhangs
+    the image (those slots hold zero radiance)."""
+    tx, _ = tiles_xy(W, H)
+    lt = np.arange(shard_tile_count(W, H, k, N))
+    t = k + lt * N
+    w = np.arange(64)
+    x = (t[:, None] % tx) * TILE + (w[None, :] & 7)
+    y = (t[:, None] // tx) * TILE + (w[None, :] >> 3)
+    idx = np.where((x < W) & (y < H), y * W + x, -1)
+    return idx.reshape(-1)
+
+
+def extract_shard(frame: np.ndarray, W: int, H: int, k: int, N: int, stride: int | None = None) -> np.ndarray:
+    """Compact shard k of a full frame [H*W, 4] (what rank k's render produces)."""
+    stride = stride or shard_stride(W, H, N)
+    lay = shard_layout(W, H, k, N)
+    out = np.zeros((stride, frame.shape[-1]), frame.dtype)
+    ok = lay >= 0
+    out[: len(lay)][ok] = frame.reshape(-1, frame.shape[-1])[lay[ok]]
+    return out
+
+
+def unshard_host(shards: np.ndarray, W: int, H: int, N: int, stride: int) -> np.ndarray:
+    """Host mirror of unshard_kernel: gathered shards [N * stride, 4] -> frame [H * W, 4]."""
+    frame = np.zeros((W * H, shards.shape[-1]), shards.dtype)
+    for k in range(N):
+        lay = shard_layout(W, H, k, N)
+        ok = lay >= 0
+        frame[lay[ok]] = shards[k * stride: k * stride + len(lay)][ok]
+    return frame
+
+
+def gather_frame(accum, gbuf, W: int, H: int, rank: int, world: int, unshard):
+    """All-gather the ranks' compact shards (torch tensors [stride, 4]) into gbuf [world * stride, 4]
+    and let rank 0 scatter them into the frame with `unshard(gbuf)`.  On RCCL the gather is one
+    all_gather_into_tensor; on gloo (no tensor-gather) a list all_gather into views of gbuf."""
+    import torch.distributed as dist
+
+    if world == 1:
+        return unshard(accum) if rank == 0 else None
+    if dist.get_backend() == "gloo":
+        stride = accum.shape[0]
+        dist.all_gather([gbuf[i * stride:(i + 1) * stride] for i in range(world)], accum)
+    else:
+        dist.all_gather_into_tensor(gbuf, accum)
+    return unshard(gbuf) if rank == 0 else None

@@ -1,0 +1,71 @@
+"""Regenerate the golden fixtures of tests/golden/ from the oracle (oracle/cpu_ref.c).
+
+The reference itself cannot be built or run here (Rust toolchain absent, nightly features, missing
+../mc_utils path dependency -- SURVEY.md §8c), so these vectors are the oracle's outputs on seeded
+synthetic inputs.  They pin the oracle against drift (tests/test_golden_cpu.py) and are the
+committed expected outputs of the GPU parity tests (tests/test_gpu_parity.py).
+
+Usage: python tests/golden/make_golden.py   (rewrites the .npz files next to this script)
+"""
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parents[1]))
+
+from oracle import cpu_ref  # noqa: E402
+from octree_pathtracing_amd import scene as S  # noqa: E402
+
+STAT_KEYS = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
+             "texel_reads", "max_path_segs")
+
+# name -> (config, width, height, spp, max_depth or None)
+RENDERS = {
+    "c1_as_is": ("C1-as-is", 256, 256, 1, None),  # sky + sun only: the reference's output today
+    "c1": ("C1", 256, 256, 1, None),
+    "tiny": ("tiny", 64, 48, 4, None),
+    "c2_small": ("C2", 160, 90, 4, None),
+    "c3_small": ("C3", 96, 54, 2, None),
+}
+
+
+def render_fixture(name):
+    cfg, W, H, spp, md = RENDERS[name]
+    sc, cam, rs = S.make_config(cfg)
+    acc, seg, st = cpu_ref.render(sc, cam, W, H, spp, max_depth=md or rs.max_depth, seed=rs.seed, forward=True,
+                                  threads=8)
+    return dict(accum=acc, segcount=seg, stats=np.array([st[k] for k in STAT_KEYS], np.uint64),
+                meta=np.array(json.dumps(dict(config=cfg, width=W, height=H, spp=spp,
+                                              max_depth=md or rs.max_depth, seed=rs.seed, forward=True))))
+
+
+def ray_fixture():
+    """Closest-hit queries on the C3 scene: primary camera rays plus rays from inside the volume."""
+    sc, cam, _ = S.make_config("C3")
+    rng = np.random.default_rng(1234)
+    n = 2048
+    o = np.empty((n, 3), np.float32)
+    o[: n // 2] = np.asarray(cam.eye, np.float32)
+    o[n // 2:] = rng.uniform(8, 248, (n // 2, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[: n // 2] = (np.float32([128, 128, 128]) - np.asarray(cam.eye, np.float32)) + rng.normal(
+        0, 60, (n // 2, 3)).astype(np.float32)
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    t, prim, nrm, steps = cpu_ref.intersect(sc, rays)
+    return dict(rays=rays, t=t, prim=prim, normal=nrm, steps=steps)
+
+
+def main():
+    for name in RENDERS:
+        np.savez_compressed(HERE / f"{name}.npz", **render_fixture(name))
+        print("wrote", name)
+    np.savez_compressed(HERE / "c3_rays.npz", **ray_fixture())
+    print("wrote c3_rays")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,74 @@
+"""The N > 1 path on the CPU: tile shards of a render all-gathered over gloo (world size 2 and 3,
+127.0.0.1 rendezvous) and scattered back into the frame must equal the unsharded render bit for
+bit, with shard sizes equal to liboctpt's octpt_shard_pixels.  The radiance comes from the oracle
+(test infrastructure); the layout, gather and unshard are the product's (distributed.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from octree_pathtracing_amd import distributed as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _frame(W, H):
+    from oracle import cpu_ref
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, _ = S.make_config("tiny")
+    acc, _, _ = cpu_ref.render(sc, cam, W, H, 2, forward=True, threads=2)
+    return acc.reshape(-1, 4)
+
+
+def _worker(rank, world, port, W, H, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from octree_pathtracing_amd import _lib
+
+        frame = _frame(W, H)  # every rank renders the same deterministic frame (pixel-keyed RNG)
+        stride = D.shard_stride(W, H, world)
+        assert _lib.load().octpt_shard_pixels(W, H, rank, world) == D.shard_tile_count(W, H, rank, world) * 64
+        shard = torch.from_numpy(D.extract_shard(frame, W, H, rank, world, stride))
+        gbuf = torch.zeros((world * stride, 4), dtype=torch.float32)
+        out = D.gather_frame(shard, gbuf, W, H, rank, world,
+                             lambda g: D.unshard_host(g.numpy(), W, H, world, stride))
+        if rank == 0:
+            q.put(bool(np.array_equal(out, frame)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 40, 24), (3, 37, 19)])
+def test_gloo_tile_gather_equals_frame(world, W, H):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
+
+
+@pytest.mark.parametrize("W,H,N", [(64, 48, 2), (70, 45, 3), (9, 17, 4), (1920, 1080, 8)])
+def test_layout_is_a_partition(W, H, N):
+    seen = np.concatenate([D.shard_layout(W, H, k, N) for k in range(N)])
+    seen = seen[seen >= 0]
+    assert len(seen) == W * H and np.array_equal(np.sort(seen), np.arange(W * H))
+    stride = D.shard_stride(W, H, N)
+    rng = np.random.default_rng(0)
+    frame = rng.random((W * H, 4), dtype=np.float32)
+    shards = np.concatenate([D.extract_shard(frame, W, H, k, N, stride) for k in range(N)])
+    assert np.array_equal(D.unshard_host(shards, W, H, N, stride), frame)
