@@ -28,7 +28,7 @@ constexpr uint32_t kCounterRing = 256;
 constexpr uint64_t kMaxChunkPaths = 128ull << 20;  // colour buffer: 2 GiB of float4 per chunk
 constexpr uint32_t kDefaultPool = 4u << 20;          // path slots in flight
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
-constexpr uint32_t kDefaultRefill = 24;              // extend: idle lanes before a wave refills
+constexpr uint32_t kDefaultRefill = 16;              // extend: idle lanes before a wave refills
 constexpr uint32_t kDefaultLeafBatch = 0;            // extend: parked lanes before a wave tests leaves (0: inline)
 
 uint32_t env_u32(const char *name, uint32_t dflt) {
@@ -79,7 +79,7 @@ struct octpt_ctx {
     double kern_ms[2] = {0.0, 0.0};
     uint64_t kern_n[2] = {0, 0};
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
-    int extend_bpc_cache[kMaxDepth + 1] = {0};
+    int extend_bpc_cache[kMaxDepth + 1][2][2] = {};
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
     size_t pool = 0, color_cap = 0;
@@ -439,8 +439,8 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
     octpt_status st = ensure_wave(ctx, pool, chunk_max);
     if (st != OCTPT_OK) return st;
-    int &bpc = ctx->extend_bpc_cache[ctx->S.depth];
-    if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S.depth);
+    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_cuboids ? 1 : 0][ctx->leaf_batch ? 1 : 0];
+    if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S, ctx->leaf_batch);
     const int grid_extend = ctx->num_cu * bpc;
     // shade maps waves to queue segments: a multiple of kSegs waves (kSegs / 4 blocks)
     const int seg_blocks = (int)(kSegs * 64u / kBlock);

@@ -139,7 +139,7 @@ hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRende
                            uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,
                              uint32_t *segcount, hipStream_t stream);
-int extend_blocks_per_cu(uint32_t depth);
+int extend_blocks_per_cu(const DevScene &S, uint32_t leaf_batch);
 hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t *last_prim,
                             const float *last_normal, uint32_t n, float *t, uint32_t *prim, float *normal,
                             uint32_t *steps, hipStream_t stream);

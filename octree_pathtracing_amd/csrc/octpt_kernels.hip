@@ -427,18 +427,21 @@ enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
 // common single-primitive leaf (one dependent load fewer).  t_accept = t_exit_w + CELL_TOL * cell_w.
+// kCuboids = false: sphere-only scenes; the slab test's temporaries then never reserve
+// registers (71 instead of 85 VGPRs in wf_extend_kernel: 7 waves/SIMD instead of 5).
+template <bool kCuboids = true>
 __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt) {
     bool found = false;
     // three correctly-rounded divides: only scenes holding cuboids pay for them (uniform branch)
     v3 inv = V(0.0f, 0.0f, 0.0f);
-    if (S.has_cuboids) inv = ray_inv_dir(r.d);
+    if (kCuboids && S.has_cuboids) inv = ray_inv_dir(r.d);
     for (uint32_t k = 0; k < lr.y; ++k) {
         const uint32_t prim = lr.y == 1u ? lr.x : S.leaf_prims[lr.x + k];
         const bool self_prim = prim == r.last_prim;
         PrimHit h;
         bool ok;
-        if (!(prim & kPrimCuboidBit)) {
+        if (!kCuboids || !(prim & kPrimCuboidBit)) {
             cnt.sph++;
             ok = sphere_test(S.spheres[prim], r, self_prim, h);
         } else {
@@ -461,7 +464,7 @@ enum : int { kStepLeaf = 3 };
 // not tested here -- the step returns kStepLeaf with (leaf, t_accept) and E.resume set; the caller
 // tests the leaf later (wave-batched) and, on a miss, calls esvo_step again, which then performs
 // the same iteration's advance without counting the iteration twice (octree_traversal.rs:142-260).
-template <bool kDefer>
+template <bool kDefer, bool kCuboids = true>
 __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const Stack &stk, Counters &cnt,
                                 uint32_t &prim, PrimHit &h, uint2 &leaf, float &t_accept) {
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
@@ -496,7 +499,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
             E.resume = true;
             return kStepLeaf;
         }
-        if (leaf_test(S, ray, slot, t_accept, prim, h, cnt)) return kStepHit;
+        if (leaf_test<kCuboids>(S, ray, slot, t_accept, prim, h, cnt)) return kStepHit;
     } else if (descend) {
         const float half = E.scale_exp2 * 0.5f;
         const v3 t_center = vadd(vscale(E.t_coef, half), t_corner);
@@ -837,6 +840,9 @@ __device__ inline unsigned long long wave_sum(uint32_t v) {
 }
 
 __device__ inline void flush_counters(const Counters &cnt, unsigned long long *stats) {
+#ifdef OCTPT_NO_STATS  // A/B builds only: every counter update becomes dead code
+    return;
+#endif
     const uint32_t vals[kStatCount] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};
 #pragma unroll
     for (int i = 0; i < kStatCount; ++i) {
@@ -1082,7 +1088,7 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #ifndef OCTPT_EXTEND_WAVES
 #define OCTPT_EXTEND_WAVES 1
 #endif
-template <bool kDefer>
+template <bool kDefer, bool kCuboids>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            uint32_t leaf_batch, unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
@@ -1141,7 +1147,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
                 pend = false;
                 uint32_t prim = kPrimNone;
                 PrimHit h;
-                if (leaf_test(S, tr, leaf, t_accept, prim, h, cnt)) {
+                if (leaf_test<kCuboids>(S, tr, leaf, t_accept, prim, h, cnt)) {
                     B.hit[pos] = make_uint4(prim, __float_as_uint(h.t),
                                             h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u), 0u);
                     cnt.steps += E.iter;
@@ -1152,7 +1158,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
         if (active && !pend) {
             uint32_t prim = kPrimNone;
             PrimHit h;
-            const int rs = esvo_step<kDefer>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
+            const int rs = esvo_step<kDefer, kCuboids>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
             if (rs == kStepLeaf) {
                 pend = true;
             } else if (rs != kStepContinue) {
@@ -1321,14 +1327,20 @@ int render_blocks_per_cu(uint32_t depth) {
     return blocks > 0 ? blocks : 1;
 }
 
-int extend_blocks_per_cu(uint32_t depth) {
-    int a = 0, b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, reinterpret_cast<const void *>(wf_extend_kernel<true>), kBlock,
-                                                     render_lds_bytes(depth)) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void *>(wf_extend_kernel<false>), kBlock,
-                                                     render_lds_bytes(depth)) != hipSuccess)
+// the extend instance a scene / leaf-batch setting launches (sphere-only scenes: no slab test)
+static const void *extend_instance(const DevScene &S, uint32_t leaf_batch) {
+    if (S.has_cuboids)
+        return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, true>)
+                          : reinterpret_cast<const void *>(wf_extend_kernel<false, true>);
+    return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, false>)
+                      : reinterpret_cast<const void *>(wf_extend_kernel<false, false>);
+}
+
+int extend_blocks_per_cu(const DevScene &S, uint32_t leaf_batch) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S, leaf_batch), kBlock,
+                                                     render_lds_bytes(S.depth)) != hipSuccess)
         return 1;
-    const int blocks = a < b ? a : b;
     return blocks > 0 ? blocks : 1;
 }
 
@@ -1349,12 +1361,10 @@ hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuff
 hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill,
                             uint32_t leaf_batch, int grid, unsigned long long *stats, hipStream_t stream) {
     // leaf_batch 0: test leaves inside the step (no deferral)
-    if (leaf_batch == 0u)
-        hipLaunchKernelGGL(wf_extend_kernel<false>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, B, q,
-                           refill, leaf_batch, stats);
-    else
-        hipLaunchKernelGGL(wf_extend_kernel<true>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, B, q,
-                           refill, leaf_batch, stats);
+    void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &leaf_batch, &stats};
+    const hipError_t e = hipLaunchKernel(extend_instance(S, leaf_batch), dim3(grid), dim3(kBlock), args,
+                                         render_lds_bytes(S.depth), stream);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

@@ -18,4 +18,7 @@ for spp in [int(x) for x in (a for a in sys.argv[2:] if not a.startswith("--"))]
     r.render_device(p, acc.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize(); dt = time.perf_counter() - t
     st = r.stats()
+    if st["segments"] == 0:  # stats compiled out (OCTPT_NO_STATS A/B builds)
+        print(f"spp {spp}: {dt*1e3:.1f} ms  (no stats)", flush=True)
+        continue
     print(f"spp {spp}: {dt*1e3:.1f} ms  {st['segments']/dt/1e6:.1f} Mrays/s  segs/path {st['segments']/st['paths']:.3f} steps/seg {st['esvo_steps']/st['segments']:.1f}", flush=True)
