@@ -197,7 +197,7 @@ struct PathState {
 struct Esvo {
     v3 t_coef, t_bias, pos;
     float t_min, t_max, h, scale_exp2;
-    uint32_t parent, pmask, idx, mirror, scale, iter;
+    uint32_t parent, pmask, idx, mirror, iter;  // scale = exponent of scale_exp2 + OCTREE_MAX_SCALE - 127
     bool resume;  // re-entering a step whose deferred leaf test missed: go straight to advance
 };
 
@@ -248,13 +248,14 @@ __device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool s
     const float disc = hh * hh - a * cc;
     if (disc < 0.0f) return false;
     const float sq = sqrtf(disc);
-    const float t0 = (hh - sq) / a;
-    const float t1 = (hh + sq) / a;
-    if (self_prim) {
-        if (r.self_inward && t1 > RAY_EPSILON) { h.t = t1; h.inside = 1u; return true; }
+    // the near root decides most tests; the far root (same formula) only when it is needed
+    if (!self_prim) {
+        const float t0 = (hh - sq) / a;
+        if (t0 > RAY_EPSILON) { h.t = t0; h.inside = 0u; return true; }
+    } else if (!r.self_inward) {
         return false;
     }
-    if (t0 > RAY_EPSILON) { h.t = t0; h.inside = 0u; return true; }
+    const float t1 = (hh + sq) / a;
     if (t1 > RAY_EPSILON) { h.t = t1; h.inside = 1u; return true; }
     return false;
 }
@@ -398,7 +399,6 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     ro = vadd(ro, V(1.0f, 1.0f, 1.0f));
     E.parent = S.root;
     E.pmask = S.root_mask;
-    E.scale = OCTREE_MAX_SCALE - 1u;
     E.scale_exp2 = 0.5f;
     const uint32_t epsb = __float_as_uint(OCTREE_EPSILON) & 0x7FFFFFFFu;
     if (fabsf(rd.x) < OCTREE_EPSILON) rd.x = __uint_as_float(epsb | (__float_as_uint(rd.x) & 0x80000000u));
@@ -500,39 +500,43 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
             return kStepLeaf;
         }
         if (leaf_test<kCuboids>(S, ray, slot, t_accept, prim, h, cnt)) return kStepHit;
-    } else if (descend) {
-        const float half = E.scale_exp2 * 0.5f;
-        const v3 t_center = vadd(vscale(E.t_coef, half), t_corner);
-        // validated trees never descend below the leaf level, so the slot is in [0, depth)
-        if (tc_max < E.h && E.scale >= OCTREE_MAX_SCALE - S.depth)
-            stk_write(stk, E.scale - (OCTREE_MAX_SCALE - S.depth), E.parent, E.t_max, E.pmask);
-        E.h = tc_max;
-        E.parent = slot.x;  // (octant, its mask)
-        E.pmask = slot.y;
-        E.scale -= 1u;
-        E.scale_exp2 = half;
-        E.idx = 0u;
-        if (t_center.x > E.t_min) { E.idx ^= 1u; E.pos.x = E.pos.x + half; }
-        if (t_center.y > E.t_min) { E.idx ^= 2u; E.pos.y = E.pos.y + half; }
-        if (t_center.z > E.t_min) { E.idx ^= 4u; E.pos.z = E.pos.z + half; }
-        E.t_max = tv_max;
-        return kStepContinue;
     }
-    // advance (:249-260)
-    uint32_t step_mask = 0u;
-    if (t_corner.x <= tc_max) { step_mask ^= 1u; E.pos.x = E.pos.x - E.scale_exp2; }
-    if (t_corner.y <= tc_max) { step_mask ^= 2u; E.pos.y = E.pos.y - E.scale_exp2; }
-    if (t_corner.z <= tc_max) { step_mask ^= 4u; E.pos.z = E.pos.z - E.scale_exp2; }
-    E.t_min = tc_max;
-    E.idx ^= step_mask;
-    if ((E.idx & step_mask) != 0u) {  // pop (:262-299)
+    // Descend (:216-244) and advance (:249-260) as one select-based update: every lane computes
+    // X = t_coef * f + t_corner with f = half for descend (X = t_center) and f = 0 otherwise
+    // (t_coef * 0 = -0 and x + -0 == x, so X = t_corner exactly), then moves pos by +half where
+    // t_center > t_min (descend) or by -scale_exp2 where t_corner <= tc_max (advance).  A wave
+    // runs both paths anyway; one shared body avoids the branch bookkeeping and phi copies.
+    const float half = E.scale_exp2 * 0.5f;
+    const float f = descend ? half : 0.0f;
+    const float Y = descend ? E.t_min : tc_max;
+    const float delta = descend ? half : -E.scale_exp2;
+    const v3 X = vadd(vscale(E.t_coef, f), t_corner);
+    // t-values are NaN-free: !(X > Y) == (X <= Y)
+    const bool cx = (X.x > Y) == descend, cy = (X.y > Y) == descend, cz = (X.z > Y) == descend;
+    if (cx) E.pos.x = E.pos.x + delta;
+    if (cy) E.pos.y = E.pos.y + delta;
+    if (cz) E.pos.z = E.pos.z + delta;
+    const uint32_t step_mask = (cx ? 1u : 0u) | (cy ? 2u : 0u) | (cz ? 4u : 0u);
+    if (descend) {
+        // validated trees never descend below the leaf level, so the slot is in [0, depth)
+        // stack slot = scale - (OCTREE_MAX_SCALE - depth) = exponent(scale_exp2) - 127 + depth
+        const int slot_i = (int)(__float_as_uint(E.scale_exp2) >> 23) - 127 + (int)S.depth;
+        if (tc_max < E.h && slot_i >= 0) stk_write(stk, (uint32_t)slot_i, E.parent, E.t_max, E.pmask);
+    }
+    E.h = descend ? tc_max : E.h;
+    E.parent = descend ? slot.x : E.parent;  // (octant, its mask)
+    E.pmask = descend ? slot.y : E.pmask;
+    E.scale_exp2 = descend ? half : E.scale_exp2;
+    E.t_max = descend ? tv_max : E.t_max;
+    E.t_min = descend ? E.t_min : tc_max;
+    E.idx = descend ? step_mask : (E.idx ^ step_mask);
+    if (!descend && (E.idx & step_mask) != 0u) {  // pop (:262-299)
         uint32_t diff = 0u;
         if (step_mask & 1u) diff |= __float_as_uint(E.pos.x) ^ __float_as_uint(E.pos.x + E.scale_exp2);
         if (step_mask & 2u) diff |= __float_as_uint(E.pos.y) ^ __float_as_uint(E.pos.y + E.scale_exp2);
         if (step_mask & 4u) diff |= __float_as_uint(E.pos.z) ^ __float_as_uint(E.pos.z + E.scale_exp2);
         const uint32_t scale = diff ? 31u - (uint32_t)__clz(diff) : 0xFFFFFFFFu;
         if (scale >= OCTREE_MAX_SCALE) return kStepMiss;
-        E.scale = scale;
         E.scale_exp2 = __uint_as_float((scale - OCTREE_MAX_SCALE + 127u) << 23);
         // slots below the finest level were never written: the oracle reads its zeroed entry
         const uint32_t base = OCTREE_MAX_SCALE - S.depth;
@@ -1102,6 +1106,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
     uint32_t seg = __builtin_amdgcn_readfirstlane(((blockIdx.x * kBlock + threadIdx.x) >> 6) % kSegs);
     uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
     bool rays_left = true;  // wave-uniform: some segment may still hold unclaimed rays
+    uint32_t segs_w = 0u;   // segments started by this wave
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     bool active = false, pend = false;
     uint32_t pos = 0u;
@@ -1122,12 +1127,12 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
                     tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk);
-                    cnt.segs++;
                     active = true;
                 } else {
                     dry = true;
                 }
             }
+            segs_w += (uint32_t)__popcll(__ballot(idle && !dry));  // uniform point: a scalar counter
             if (__ballot(dry) != 0ull) {  // segment drained: lane j checks segment j, the wave moves on
                 const uint32_t j = threadIdx.x & 63u;
                 const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, j)) < B.ctrl[ctr_count(q, j)]);
@@ -1172,6 +1177,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
             }
         }
     }
+    cnt.segs = (threadIdx.x & 63u) == 0u ? segs_w : 0u;  // flush_counters sums over the wave's lanes
     flush_counters(cnt, stats);
 }
 
