@@ -660,20 +660,30 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         free_scene(ctx);
         DevScene S{};
-        // packed child slots: one 8-byte load per descend / leaf visit
-        std::vector<uint2> child((size_t)d->octant_count * 8, make_uint2(0u, 0u));
+        // sparse packed child slots: octant n's present children are stored
+        // contiguously from base[n] in child order; child i is at base[n] + popcount(mask & (2^i - 1)).
+        // One 8-byte load per descend / leaf visit yields the child's own base and mask.
+        std::vector<uint32_t> base(d->octant_count);
+        size_t n_slots = 0;
+        for (uint32_t n = 0; n < d->octant_count; ++n) {
+            base[n] = (uint32_t)n_slots;
+            n_slots += (size_t)__builtin_popcount(d->octants[n].child_mask & 0xFFu);
+        }
+        if (n_slots >= 0xFFFFFFFFull) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree too large");
+        std::vector<uint2> child(std::max<size_t>(n_slots, 1), make_uint2(0u, 0u));
         for (uint32_t n = 0; n < d->octant_count; ++n) {
             const octpt_octant &o = d->octants[n];
+            uint32_t k = base[n];
             for (int i = 0; i < 8; ++i) {
                 const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
                 if (!present) continue;
                 const uint32_t v = o.children[i];
                 if (!leaf) {
-                    child[(size_t)n * 8 + i] = make_uint2(v, d->octants[v].child_mask);
+                    child[k++] = make_uint2(base[v], d->octants[v].child_mask);
                 } else if (d->leaf_count[v] == 1) {  // single-primitive leaf: the prim id itself
-                    child[(size_t)n * 8 + i] = make_uint2(d->leaf_prims[d->leaf_first[v]], 1u);
+                    child[k++] = make_uint2(d->leaf_prims[d->leaf_first[v]], 1u);
                 } else {
-                    child[(size_t)n * 8 + i] = make_uint2(d->leaf_first[v], d->leaf_count[v]);
+                    child[k++] = make_uint2(d->leaf_first[v], d->leaf_count[v]);
                 }
             }
         }
@@ -748,9 +758,9 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         HIP_TRY(ctx, upload(ctx, texs.data(), texs.size(), &d_texs));
         HIP_TRY(ctx, upload(ctx, texels.data(), texels.size(), &d_texels));
         S.node_child = d_child;
-        S.root = d->root;
+        S.root = base[d->root];  // traversal "parent" values are child-array bases
         S.root_mask = d->octants[d->root].child_mask;
-        S.node0_mask = d->octants[0].child_mask;
+        S.node0_mask = d->octants[0].child_mask;  // base[0] == 0: a zeroed stack entry reads octant 0
         S.depth = d->depth;
         S.n_octants = d->octant_count;
         S.has_cuboids = d->cuboid_count ? 1u : 0u;

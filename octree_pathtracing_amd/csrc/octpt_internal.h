@@ -46,10 +46,11 @@ struct DevSun {
 };
 
 struct DevScene {
-    // 8 packed child slots per octant: octant child = (index, its child_mask),
-    // leaf child = (first leaf prim, prim count), empty = (0, 0)
+    // sparse packed child slots: an octant's present children are contiguous from
+    // its base; octant child = (its base, its child_mask), leaf child = (prim id, 1) or
+    // (first leaf prim, prim count)
     const uint2 *node_child;
-    uint32_t root, root_mask, node0_mask, depth, n_octants;
+    uint32_t root, root_mask, node0_mask, depth, n_octants;  // root = the root octant's base
     uint32_t has_cuboids;
     float octree_scale;             // 2^-depth
     float inv_octree_scale;         // 2^depth (x / 2^-depth == x * 2^depth exactly)

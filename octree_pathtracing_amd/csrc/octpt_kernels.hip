@@ -239,25 +239,28 @@ struct PrimHit {
     float nsgn;
 };
 
-// Sphere::hit restated (sphere.rs:33-57) + root selection [C2]
+// Sphere::hit restated (sphere.rs:33-57) + root selection [C2].  Straight-line: the near root is
+// computed for every lane (the common case), the far root only for lanes that need it (origin
+// inside the sphere, or re-entering the primitive the ray left).
 __device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool self_prim, PrimHit &h) {
     const v3 oc = vsub(V(sp.x, sp.y, sp.z), r.o);
     const float a = vdot(r.d, r.d);
     const float hh = vdot(r.d, oc);
     const float cc = vdot(oc, oc) - sp.w * sp.w;
     const float disc = hh * hh - a * cc;
-    if (disc < 0.0f) return false;
-    const float sq = sqrtf(disc);
-    // the near root decides most tests; the far root (same formula) only when it is needed
-    if (!self_prim) {
-        const float t0 = (hh - sq) / a;
-        if (t0 > RAY_EPSILON) { h.t = t0; h.inside = 0u; return true; }
-    } else if (!r.self_inward) {
-        return false;
+    const bool real = disc >= 0.0f;
+    const float sq = sqrtf(disc);  // NaN when disc < 0: unused then
+    const float t0 = (hh - sq) / a;
+    const bool near_ok = real && !self_prim && t0 > RAY_EPSILON;
+    float t1 = 0.0f;
+    bool far_ok = false;
+    if (real && !near_ok && (!self_prim || r.self_inward)) {
+        t1 = (hh + sq) / a;
+        far_ok = t1 > RAY_EPSILON;
     }
-    const float t1 = (hh + sq) / a;
-    if (t1 > RAY_EPSILON) { h.t = t1; h.inside = 1u; return true; }
-    return false;
+    h.t = near_ok ? t0 : t1;
+    h.inside = near_ok ? 0u : 1u;
+    return near_ok || far_ok;
 }
 
 __device__ __forceinline__ float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6f : 1.0f / d; }
@@ -429,29 +432,42 @@ enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 // common single-primitive leaf (one dependent load fewer).  t_accept = t_exit_w + CELL_TOL * cell_w.
 // kCuboids = false: sphere-only scenes; the slab test's temporaries then never reserve
 // registers (71 instead of 85 VGPRs in wf_extend_kernel: 7 waves/SIMD instead of 5).
+template <bool kCuboids>
+__device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, uint32_t prim, v3 inv, float t_accept,
+                                          PrimHit &h, Counters &cnt) {
+    const bool self_prim = prim == r.last_prim;
+    bool ok;
+    if (!kCuboids || !(prim & kPrimCuboidBit)) {
+        cnt.sph++;
+        ok = sphere_test(S.spheres[prim], r, self_prim, h);
+    } else {
+        cnt.cub++;
+        const uint32_t ci = prim & ~kPrimCuboidBit;
+        ok = cuboid_test(S.cub_min[ci], S.cub_max[ci], r, inv, self_prim, h);
+    }
+    return ok && h.t <= t_accept;
+}
+
+// kCuboids = false: sphere-only scenes; the slab test's temporaries then never reserve
+// registers (70 instead of 85 VGPRs in wf_extend_kernel: 7 waves/SIMD instead of 5).
+// The first primitive is tested straight-line (leaves hold 1.02 primitives on average); the
+// rest of a multi-primitive list in a loop, keeping the closest accepted hit.
 template <bool kCuboids = true>
 __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt) {
-    bool found = false;
     // three correctly-rounded divides: only scenes holding cuboids pay for them (uniform branch)
     v3 inv = V(0.0f, 0.0f, 0.0f);
     if (kCuboids && S.has_cuboids) inv = ray_inv_dir(r.d);
-    for (uint32_t k = 0; k < lr.y; ++k) {
-        const uint32_t prim = lr.y == 1u ? lr.x : S.leaf_prims[lr.x + k];
-        const bool self_prim = prim == r.last_prim;
-        PrimHit h;
-        bool ok;
-        if (!kCuboids || !(prim & kPrimCuboidBit)) {
-            cnt.sph++;
-            ok = sphere_test(S.spheres[prim], r, self_prim, h);
-        } else {
-            cnt.cub++;
-            const uint32_t ci = prim & ~kPrimCuboidBit;
-            ok = cuboid_test(S.cub_min[ci], S.cub_max[ci], r, inv, self_prim, h);
-        }
-        if (ok && h.t <= t_accept && (!found || h.t < best.t)) {
-            best = h;
-            best_prim = prim;
+    uint32_t prim = lr.x;
+    if (lr.y != 1u) prim = S.leaf_prims[lr.x];
+    bool found = prim_test<kCuboids>(S, r, prim, inv, t_accept, best, cnt);
+    if (found) best_prim = prim;
+    for (uint32_t k = 1; k < lr.y; ++k) {
+        const uint32_t p = S.leaf_prims[lr.x + k];
+        PrimHit hk;
+        if (prim_test<kCuboids>(S, r, p, inv, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
+            best = hk;
+            best_prim = p;
             found = true;
         }
     }
@@ -489,7 +505,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const bool take_leaf = live && is_leaf && E.t_min >= 0.0f && !resume;
     const bool descend = live && !is_leaf && E.t_min <= tv_max;
     uint2 slot = make_uint2(0u, 0u);
-    if (take_leaf || descend) slot = S.node_child[8u * E.parent + cidx];
+    if (take_leaf || descend) slot = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx) - 1u))];
     if (take_leaf) {
         // x / 2^-depth == x * 2^depth exactly (the oracle divides)
         const float cell_w = E.scale_exp2 * S.inv_octree_scale;
