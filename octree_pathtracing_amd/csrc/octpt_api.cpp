@@ -25,7 +25,9 @@ using namespace octpt;
 namespace {
 
 constexpr uint32_t kCounterRing = 256;
-constexpr uint64_t kMaxChunkPaths = 128ull << 20;  // colour buffer: 2 GiB of float4 per chunk
+constexpr uint64_t kMaxChunkPaths = 1ull << 30;    // colour buffer: up to 16 GiB of float4 per chunk
+                                                    // (C3 = 530 M paths = one chunk: one drain tail)
+constexpr uint32_t kLookahead = 3;                  // host steering: iterations queued ahead of the check
 constexpr uint32_t kDefaultPool = 4u << 20;          // path slots in flight
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
 constexpr uint32_t kDefaultRefill = 16;              // extend: idle lanes before a wave refills
@@ -85,9 +87,10 @@ struct octpt_ctx {
     size_t pool = 0, color_cap = 0;
     std::vector<void *> wave_allocs;
     void *color_alloc = nullptr;
-    uint32_t *h_count = nullptr;  // pinned: the segment counters of each queue, 2 x kCountSpan words
-    hipEvent_t count_ev[2] = {nullptr, nullptr};
+    uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
+    hipEvent_t count_ev[kLookahead + 1] = {};
     uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill, leaf_batch = kDefaultLeafBatch;
+    uint64_t chunk_cap = kMaxChunkPaths;  // (pixel, sample) items per chunk (OCTPT_CHUNK: tests)
     // one asynchronous frame may be in flight; device-touching calls join it first
     octpt_frame *inflight = nullptr;
 };
@@ -360,7 +363,7 @@ size_t seg_cap_for(size_t pool) { return ((pool + 63) / 64 + kSegs - 1) / kSegs 
 
 octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
     if (!ctx->h_count) {
-        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), 2 * kCountSpan * sizeof(uint32_t),
+        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), (kLookahead + 1) * kCountSpan * sizeof(uint32_t),
                                    hipHostMallocDefault));
         for (auto &ev : ctx->count_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
@@ -434,7 +437,7 @@ octpt_status enqueue_megakernel(octpt_ctx *ctx, const DevRender &R, float4 *d_ac
 octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s,
                                const std::atomic<bool> *cancel) {
     const uint64_t n_px = R.total_items;
-    const uint32_t chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, kMaxChunkPaths / n_px));
+    const uint32_t chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, ctx->chunk_cap / n_px));
     const uint64_t chunk_max = (uint64_t)chunk_spp * n_px;
     const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
     octpt_status st = ensure_wave(ctx, pool, chunk_max);
@@ -464,15 +467,21 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
             HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, grid_shade, ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 1, ev)) != OCTPT_OK) return st;
-            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_count + q * kCountSpan, B.ctrl + ctr_count(q ^ 1u, 0),
+            // snapshot of the queue iteration `it` produced; the host checks the snapshot of
+            // iteration it - kLookahead, so the GPU always has kLookahead iterations queued (an
+            // iteration over an empty queue exits at once).  The queue only empties once every
+            // chunk item is claimed: finished paths regenerate in the same shade pass.
+            const uint32_t slot = it % (kLookahead + 1);
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_count + slot * kCountSpan, B.ctrl + ctr_count(q ^ 1u, 0),
                                         kCountSpan * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-            HIP_TRY(ctx, hipEventRecord(ctx->count_ev[q], s));
-            if (it >= 1) {
-                HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[q ^ 1u]));
-                const uint32_t *h = ctx->h_count + (q ^ 1u) * kCountSpan;
+            HIP_TRY(ctx, hipEventRecord(ctx->count_ev[slot], s));
+            if (it >= kLookahead) {
+                const uint32_t old = (it - kLookahead) % (kLookahead + 1);
+                HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[old]));
+                const uint32_t *h = ctx->h_count + old * kCountSpan;
                 uint64_t queued = 0;
                 for (uint32_t k = 0; k < kSegs; ++k) queued += h[k * kCtrStride];
-                if (queued == 0u) break;  // iteration `it` had nothing to do
+                if (queued == 0u) break;  // iteration it - kLookahead + 1 onwards had nothing to do
             }
         }
         HIP_TRY(ctx, launch_wf_resolve(Rc, B, Rc.spp_count, d_accum, d_seg, s));
@@ -601,6 +610,7 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->device = device;
     ctx->num_cu = prop.multiProcessorCount;
     ctx->pool_cap = env_u32("OCTPT_POOL", kDefaultPool);
+    ctx->chunk_cap = std::min<uint64_t>(env_u32("OCTPT_CHUNK", (uint32_t)kMaxChunkPaths), kMaxChunkPaths);
     ctx->refill = std::min<uint32_t>(env_u32("OCTPT_REFILL", kDefaultRefill), 64u);
     ctx->leaf_batch = std::min<uint32_t>(env_u32("OCTPT_LEAF_BATCH", kDefaultLeafBatch), 64u);
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);

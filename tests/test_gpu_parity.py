@@ -332,7 +332,7 @@ def test_megakernel_equals_wavefront(torch_cuda, renderer, name, res):
 
 
 def test_wavefront_small_pool_many_chunks(torch_cuda, renderer):
-    """Pool much smaller than the work (path regeneration) and ragged tiles."""
+    """Pool much smaller than the work (path regeneration), 3 chunks (OCTPT_CHUNK) and ragged tiles."""
     import os
     from octree_pathtracing_amd import scene as S
     from octree_pathtracing_amd.renderer import HipRenderer
@@ -342,12 +342,13 @@ def test_wavefront_small_pool_many_chunks(torch_cuda, renderer):
     ref = gpu_render(torch_cuda, renderer, sc, cam, rs)
     os.environ["OCTPT_POOL"] = "100"
     os.environ["OCTPT_REFILL"] = "1"
+    os.environ["OCTPT_CHUNK"] = "2000"  # 960 tile pixels: 2 spp per chunk
     try:
         small = HipRenderer(0)
         out = gpu_render(torch_cuda, small, sc, cam, rs)
         small.close()
     finally:
-        del os.environ["OCTPT_POOL"], os.environ["OCTPT_REFILL"]
+        del os.environ["OCTPT_POOL"], os.environ["OCTPT_REFILL"], os.environ["OCTPT_CHUNK"]
     assert np.array_equal(ref[0], out[0]) and np.array_equal(ref[1], out[1])
 
 
