@@ -1,4 +1,3 @@
 set -o pipefail
-timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
-tail -1 gpurun_out/t.log
-echo "== C3 64/256"; timeout -k 10 120 python scripts/spp_sweep.py C3 64 256 2>&1 | grep spp || exit 1
+echo "== base"; timeout -k 10 120 python scripts/spp_sweep.py C3 64 --ktime 2>&1 | grep spp || exit 1
+echo "== xcdmix"; OCTPT_LIB=build_variants/xcdmix/liboctpt.so timeout -k 10 120 python scripts/spp_sweep.py C3 64 --ktime 2>&1 | grep spp || exit 1

@@ -6,14 +6,17 @@ from octree_pathtracing_amd import scene as S
 from octree_pathtracing_amd.renderer import HipRenderer
 
 sc, cam, rs = S.make_config(sys.argv[1] if len(sys.argv) > 1 else "C3")
+import os
+rs.max_depth = int(os.environ.get("MAXDEPTH", rs.max_depth))  # experiments: primary-only = 1
 r = HipRenderer(0)
+r.max_depth = rs.max_depth
 r.set_scene(sc); r.set_camera(cam)
 W, H = rs.width, rs.height
 acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"); acc[:, 3] = 1
 mega = "--mega" in sys.argv
 for spp in [int(x) for x in (a for a in sys.argv[2:] if not a.startswith("--"))] or [4, 16, 64, 256]:
     r.reset_stats()
-    p = r.params(W, H, 0, spp, megakernel=mega)
+    p = r.params(W, H, 0, spp, megakernel=mega, kernel_timing="--ktime" in sys.argv)
     torch.cuda.synchronize(); t = time.perf_counter()
     r.render_device(p, acc.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize(); dt = time.perf_counter() - t
@@ -21,4 +24,5 @@ for spp in [int(x) for x in (a for a in sys.argv[2:] if not a.startswith("--"))]
     if st["segments"] == 0:  # stats compiled out (OCTPT_NO_STATS A/B builds)
         print(f"spp {spp}: {dt*1e3:.1f} ms  (no stats)", flush=True)
         continue
-    print(f"spp {spp}: {dt*1e3:.1f} ms  {st['segments']/dt/1e6:.1f} Mrays/s  segs/path {st['segments']/st['paths']:.3f} steps/seg {st['esvo_steps']/st['segments']:.1f}", flush=True)
+    kt = f"  extend {st['extend_ms']:.1f} ms shade {st['shade_ms']:.1f} ms" if st["extend_launches"] else ""
+    print(f"spp {spp}: {dt*1e3:.1f} ms  {st['segments']/dt/1e6:.1f} Mrays/s  segs/path {st['segments']/st['paths']:.3f} steps/seg {st['esvo_steps']/st['segments']:.1f}{kt}", flush=True)
