@@ -339,6 +339,57 @@ def primitive_materials(scene: Scene) -> dict:
     return ids
 
 
+def procedural_terrain(seed: int, w: int = 1024, h: int = 512) -> np.ndarray:
+    """Deterministic stand-in for a photographic colour map: bilinear value noise (4 octaves)
+    mapped to water / land / rock / snow colours, RGBA8, opaque."""
+    acc = np.zeros((h, w), np.float32)
+    for o, (gx, gy) in enumerate([(8, 4), (16, 8), (32, 16), (64, 32)]):
+        g = scene_uniform(seed, 100 + o, (gy + 1) * (gx + 1)).reshape(gy + 1, gx + 1)
+        ys = np.linspace(0, gy, h, endpoint=False, dtype=np.float32)
+        xs = np.linspace(0, gx, w, endpoint=False, dtype=np.float32)
+        y0, x0 = ys.astype(np.int64), xs.astype(np.int64)
+        fy, fx = (ys - y0)[:, None], (xs - x0)[None, :]
+        v = (g[y0][:, x0] * (1 - fx) + g[y0][:, x0 + 1] * fx) * (1 - fy) + \
+            (g[y0 + 1][:, x0] * (1 - fx) + g[y0 + 1][:, x0 + 1] * fx) * fy
+        acc += v / (2 ** o)
+    acc /= acc.max()
+    pal = np.array([(20, 40, 120), (30, 90, 170), (60, 140, 60), (120, 110, 60), (150, 140, 130), (240, 240, 245)],
+                   np.float32)
+    stops = np.array([0.0, 0.45, 0.5, 0.65, 0.8, 1.0], np.float32)
+    rgb = np.stack([np.interp(acc, stops, pal[:, c]) for c in range(3)], -1)
+    out = np.empty((h, w, 4), np.uint8)
+    out[..., :3] = np.clip(rgb, 0, 255).astype(np.uint8)
+    out[..., 3] = 255
+    return out
+
+
+def procedural_atlas(seed: int, tiles: int = 16, tile: int = 16) -> np.ndarray:
+    """A 16x16 atlas of 16x16-texel tiles (block-texture layout) with per-tile colour and texel
+    noise; about 2 % of the texels are fully transparent (alpha 0: the transparent-texel path, C4)."""
+    n = tiles * tile
+    base = (scene_uniform(seed, 200, tiles * tiles * 3).reshape(tiles, tiles, 3) * 200 + 40)
+    noise = scene_uniform(seed, 201, n * n).reshape(n, n) * 40 - 20
+    rgb = np.repeat(np.repeat(base, tile, 0), tile, 1) + noise[..., None]
+    out = np.empty((n, n, 4), np.uint8)
+    out[..., :3] = np.clip(rgb, 0, 255).astype(np.uint8)
+    out[..., 3] = np.where(scene_uniform(seed, 202, n * n).reshape(n, n) < 0.02, 0, 255).astype(np.uint8)
+    return out
+
+
+def textured_materials(scene: Scene, seed: int) -> dict:
+    """primitive_materials with the diffuse set replaced by image-textured materials (C4: a
+    1024x512 colour map and a 256x256 block atlas)."""
+    ids = primitive_materials(scene)
+    scene.textures.append(Texture.image(procedural_terrain(seed)))
+    scene.materials.append(Material(texture_index=len(scene.textures) - 1))
+    terrain = len(scene.materials) - 1
+    scene.textures.append(Texture.image(procedural_atlas(seed)))
+    scene.materials.append(Material(texture_index=len(scene.textures) - 1))
+    atlas = len(scene.materials) - 1
+    ids["diffuse"] = [terrain, atlas]
+    return ids
+
+
 def _assign_materials(ids, seed, n, stream=7):
     """70% diffuse, 15% metal, 10% glossy, 5% glass."""
     u = scene_uniform(seed, stream, n)
@@ -405,7 +456,7 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
         cam = Camera.look_at((128.0, 150.0, -110.0), (128.0, 128.0, 128.0))
         rs = RenderSettings(1920, 1080, 256, seed=seed)
     elif name == "C4":
-        ids = primitive_materials(sc)
+        ids = textured_materials(sc, seed)
         depth = 10
         n = 50_000
         sc.spheres = random_spheres(seed, n, 1024.0, 0.5, 4.0)

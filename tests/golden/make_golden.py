@@ -29,6 +29,7 @@ RENDERS = {
     "tiny": ("tiny", 64, 48, 4, None),
     "c2_small": ("C2", 160, 90, 4, None),
     "c3_small": ("C3", 96, 54, 2, None),
+    "c4_small": ("C4", 64, 36, 2, None),  # cuboids + image textures (procedural, scene.py)
 }
 
 

@@ -11,7 +11,7 @@ from oracle import cpu_ref
 from octree_pathtracing_amd import scene as S
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
-RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small"]
+RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small"]
 STAT_KEYS = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
              "texel_reads", "max_path_segs")
 

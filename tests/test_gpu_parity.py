@@ -88,7 +88,7 @@ def assert_parity(gpu, ref, tag):
 
 
 @pytest.mark.parametrize("name,res", [("tiny", None), ("C1", None), ("C1-as-is", None), ("C2", (160, 90, 8)),
-                                      ("C3", (192, 108, 2))])
+                                      ("C3", (192, 108, 2)), ("C4", (128, 72, 2))])
 def test_render_parity(torch_cuda, renderer, name, res):
     from octree_pathtracing_amd import scene as S
 
@@ -355,7 +355,7 @@ def test_wavefront_small_pool_many_chunks(torch_cuda, renderer):
 GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
 
 
-@pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small"])
+@pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small"])
 def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     """GPU render vs the committed oracle fixture (tests/golden/make_golden.py): exact per-pixel
     segment counts and work totals, radiance within REL_TOL_FORWARD."""
