@@ -704,12 +704,13 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
             sph[s] = make_float4(x.center[0], x.center[1], x.center[2], x.radius);
             sph_mat[s] = x.material;
         }
-        std::vector<float4> cmin(d->cuboid_count), cmax(d->cuboid_count);
+        std::vector<float4> cmin(d->cuboid_count);
+        std::vector<float2> cmax(d->cuboid_count);
         std::vector<uint32_t> cmat((size_t)d->cuboid_count * 6);
         for (uint32_t c = 0; c < d->cuboid_count; ++c) {
             const octpt_cuboid &x = d->cuboids[c];
-            cmin[c] = make_float4(x.min[0], x.min[1], x.min[2], 0.0f);
-            cmax[c] = make_float4(x.max[0], x.max[1], x.max[2], 0.0f);
+            cmin[c] = make_float4(x.min[0], x.min[1], x.min[2], x.max[0]);
+            cmax[c] = make_float2(x.max[1], x.max[2]);
             std::memcpy(&cmat[(size_t)c * 6], x.face_material, 24);
         }
         float lf[256];
@@ -753,7 +754,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         }
         uint32_t *d_prims, *d_sph_mat, *d_cmat;
         uint2 *d_child;
-        float4 *d_sph, *d_cmin, *d_cmax;
+        float4 *d_sph, *d_cmin;
+        float2 *d_cmax;
         DevMaterial *d_mats;
         DevTexture *d_texs;
         uint8_t *d_texels;
@@ -779,8 +781,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.leaf_prims = d_prims;
         S.spheres = d_sph;
         S.sphere_mat = d_sph_mat;
-        S.cub_min = d_cmin;
-        S.cub_max = d_cmax;
+        S.cub_a = d_cmin;
+        S.cub_b = d_cmax;
         S.cub_mat = d_cmat;
         S.mats = d_mats;
         S.texs = d_texs;

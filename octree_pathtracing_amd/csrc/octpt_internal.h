@@ -57,8 +57,8 @@ struct DevScene {
     const uint32_t *leaf_prims;
     const float4 *spheres;          // (cx, cy, cz, r)
     const uint32_t *sphere_mat;
-    const float4 *cub_min;          // (x, y, z, -)
-    const float4 *cub_max;
+    const float4 *cub_a;            // (min.x, min.y, min.z, max.x)
+    const float2 *cub_b;            // (max.y, max.z): 24 B per box in two loads, no padding lanes
     const uint32_t *cub_mat;        // 6 per cuboid
     const DevMaterial *mats;
     const DevTexture *texs;

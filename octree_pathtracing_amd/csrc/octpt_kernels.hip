@@ -273,10 +273,13 @@ __device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const Trac
                                             PrimHit &h) {
     const v3 tb = vmul(vsub(V(bmin.x, bmin.y, bmin.z), r.o), inv);
     const v3 tt = vmul(vsub(V(bmax.x, bmax.y, bmax.z), r.o), inv);
-    const v3 mins = V(fmn(tb.x, tt.x), fmn(tb.y, tt.y), fmn(tb.z, tt.z));
-    const v3 maxs = V(fmx(tb.x, tt.x), fmx(tb.y, tt.y), fmx(tb.z, tt.z));
-    float t0 = vmax3(mins);
-    const float t1 = vmin3(maxs);
+    // inv is finite (clamped to +-1e6) and so are tb, tt: no NaN reaches these.  A +-0 can differ
+    // from the oracle's a < b ? a : b only in sign, and a zero t is never accepted (t > EPSILON)
+    // while the axis tests below compare with ==, so v_min3 / v_max3 give identical results.
+    const v3 mins = V(tmn(tb.x, tt.x), tmn(tb.y, tt.y), tmn(tb.z, tt.z));
+    const v3 maxs = V(tmx(tb.x, tt.x), tmx(tb.y, tt.y), tmx(tb.z, tt.z));
+    float t0 = tmax3(mins);
+    const float t1 = tmin3(maxs);
     if (!isfinite(t0)) t0 = t1;
     if (t1 < t0) return false;
     uint32_t inside;
@@ -322,7 +325,9 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
         uv_ready = false;  // sphere uv only feeds image textures (computed lazily below)
     } else {
         const uint32_t ci = prim & ~kPrimCuboidBit;
-        const float4 bmin = S.cub_min[ci], bmax = S.cub_max[ci];
+        const float4 ca = S.cub_a[ci];
+        const float2 cb = S.cub_b[ci];
+        const float4 bmin = make_float4(ca.x, ca.y, ca.z, 0.0f), bmax = make_float4(ca.w, cb.x, cb.y, 0.0f);
         n = V(0.0f, 0.0f, 0.0f);
         if (h.axis == 0u) n.x = h.nsgn; else if (h.axis == 1u) n.y = h.nsgn; else n.z = h.nsgn;
         const float ex = bmax.x - bmin.x, ey = bmax.y - bmin.y, ez = bmax.z - bmin.z;
@@ -443,7 +448,9 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
     } else {
         cnt.cub++;
         const uint32_t ci = prim & ~kPrimCuboidBit;
-        ok = cuboid_test(S.cub_min[ci], S.cub_max[ci], r, inv, self_prim, h);
+        const float4 ca = S.cub_a[ci];
+        const float2 cb = S.cub_b[ci];
+        ok = cuboid_test(make_float4(ca.x, ca.y, ca.z, 0.0f), make_float4(ca.w, cb.x, cb.y, 0.0f), r, inv, self_prim, h);
     }
     return ok && h.t <= t_accept;
 }
@@ -1198,7 +1205,10 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
 }
 
 // shade: one lane per traced ray (grid-stride, wave-uniform trip count)
-__global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, DevCamera C, DevRender R, WaveBuffers B,
+#ifndef OCTPT_SHADE_WAVES
+#define OCTPT_SHADE_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene S, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items,
                                                           unsigned long long *__restrict__ stats) {
     // wave w shades segment w % kSegs of queue q (grid: a multiple of kSegs waves) and appends
