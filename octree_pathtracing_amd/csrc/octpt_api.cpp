@@ -81,7 +81,7 @@ struct octpt_ctx {
     double kern_ms[2] = {0.0, 0.0};
     uint64_t kern_n[2] = {0, 0};
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
-    int extend_bpc_cache[kMaxDepth + 1][2][2] = {};
+    int extend_bpc_cache[kMaxDepth + 1][2][3] = {};
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
     size_t pool = 0, color_cap = 0;
@@ -442,7 +442,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
     octpt_status st = ensure_wave(ctx, pool, chunk_max);
     if (st != OCTPT_OK) return st;
-    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_cuboids ? 1 : 0][ctx->leaf_batch ? 1 : 0];
+    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_cuboids ? 1 : 0][ctx->leaf_batch == kLeafSplit ? 2 : (ctx->leaf_batch ? 1 : 0)];
     if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S, ctx->leaf_batch);
     const int grid_extend = ctx->num_cu * bpc;
     // shade maps waves to queue segments: a multiple of kSegs waves (kSegs / 4 blocks)
@@ -613,6 +613,9 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->chunk_cap = std::min<uint64_t>(env_u32("OCTPT_CHUNK", (uint32_t)kMaxChunkPaths), kMaxChunkPaths);
     ctx->refill = std::min<uint32_t>(env_u32("OCTPT_REFILL", kDefaultRefill), 64u);
     ctx->leaf_batch = std::min<uint32_t>(env_u32("OCTPT_LEAF_BATCH", kDefaultLeafBatch), 64u);
+    if (const char *m = std::getenv("OCTPT_EXTEND")) {  // extend variant: "split" = wave-specialised
+        if (std::string(m) == "split") ctx->leaf_batch = kLeafSplit;
+    }
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);

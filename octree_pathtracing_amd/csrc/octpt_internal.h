@@ -128,6 +128,10 @@ enum StatIndex {
 constexpr uint32_t kStatRow = 32;
 constexpr uint32_t kStatWords = kSegs * kStatRow;
 
+// extend variants (launch_wf_extend's leaf_batch): 0 leaf tests inline, 1..64 wave-local deferral,
+// kLeafSplit the wave-specialised kernel (3 traversal waves + 1 leaf-test wave per block)
+constexpr uint32_t kLeafSplit = 0xFFFFu;
+
 // kernel launchers (octpt_kernels.hip)
 hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
                          uint32_t *segcount, uint32_t *counter, unsigned long long *stats, int grid,

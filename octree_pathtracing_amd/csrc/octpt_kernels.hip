@@ -179,10 +179,14 @@ struct TraceRay {
 };
 
 // ESVO stack in LDS: (octant, t_max) + the octant's child mask, [slot][thread] rows
-struct Stack {
+// per-lane ESVO stack in LDS: entry (parent base, t_max) and 16-bit mask per scale, lanes
+// interleaved with stride kStride (the threads of the block that traverse)
+template <uint32_t kStride>
+struct StackT {
     uint2 *e;
     uint16_t *m;
 };
+using Stack = StackT<kBlock>;
 
 // Path state between segments (Ray + HitRecord of ray/mod.rs:16-23, hittable/mod.rs:53-84,
 // plus the forward throughput T / radiance L of the kernel's accumulation order).
@@ -375,15 +379,17 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
 // ---------------------------------------------------------------------------
 // ESVO (octree_traversal.rs:54-302) split into setup + one iteration
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void stk_write(const Stack &stk, uint32_t slot, uint32_t node, float t, uint32_t mask) {
-    stk.e[slot * kBlock] = make_uint2(node, __float_as_uint(t));
-    stk.m[slot * kBlock] = (uint16_t)mask;
+template <uint32_t kS>
+__device__ __forceinline__ void stk_write(const StackT<kS> &stk, uint32_t slot, uint32_t node, float t, uint32_t mask) {
+    stk.e[slot * kS] = make_uint2(node, __float_as_uint(t));
+    stk.m[slot * kS] = (uint16_t)mask;
 }
 
-__device__ __forceinline__ Stack stack_of(uint2 *lds, uint32_t depth) {
-    Stack s;
+template <uint32_t kS = kBlock>
+__device__ __forceinline__ StackT<kS> stack_of(uint2 *lds, uint32_t depth) {
+    StackT<kS> s;
     s.e = lds + threadIdx.x;
-    s.m = reinterpret_cast<uint16_t *>(lds + (size_t)depth * kBlock) + threadIdx.x;
+    s.m = reinterpret_cast<uint16_t *>(lds + (size_t)depth * kS) + threadIdx.x;
     return s;
 }
 
@@ -396,7 +402,8 @@ __device__ __forceinline__ TraceRay make_trace_ray(const DevScene &S, v3 o, v3 d
     return t;
 }
 
-__device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const Stack &stk) {
+template <uint32_t kS>
+__device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk) {
     const float osc = S.octree_scale;
     // The reference zero-initialises the stack (octree_traversal.rs:69-70).  ESVO only pops to a
     // scale it pushed during the same ray (a push is skipped only when the entry already holds the
@@ -487,8 +494,8 @@ enum : int { kStepLeaf = 3 };
 // not tested here -- the step returns kStepLeaf with (leaf, t_accept) and E.resume set; the caller
 // tests the leaf later (wave-batched) and, on a miss, calls esvo_step again, which then performs
 // the same iteration's advance without counting the iteration twice (octree_traversal.rs:142-260).
-template <bool kDefer, bool kCuboids = true>
-__device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const Stack &stk, Counters &cnt,
+template <bool kDefer, bool kCuboids = true, uint32_t kS = kBlock>
+__device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk, Counters &cnt,
                                 uint32_t &prim, PrimHit &h, uint2 &leaf, float &t_accept) {
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
     const bool resume = kDefer && E.resume;
@@ -566,8 +573,8 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         uint2 e = make_uint2(0u, 0u);
         uint32_t em = S.node0_mask;
         if (scale >= base) {
-            e = stk.e[(scale - base) * kBlock];
-            em = stk.m[(scale - base) * kBlock];
+            e = stk.e[(scale - base) * kS];
+            em = stk.m[(scale - base) * kS];
         }
         E.parent = e.x;
         E.pmask = em;
@@ -1204,6 +1211,168 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
     flush_counters(cnt, stats);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-specialised extend: waves 0-2 of a block traverse, wave 3 runs the leaf
+// primitive tests.  A traversal lane reaching a leaf posts (ray position, leaf slot, t_accept)
+// into its LDS job record and its wave keeps stepping the other lanes; the leaf wave gathers the
+// posted jobs of all 192 traversal lanes, tests them with the lanes of one wave, and answers.  A
+// miss resumes ESVO with the same iteration's advance (esvo_step kDefer), so traversal order,
+// counters and results are exactly those of wf_extend_kernel.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kTravLanes = 192;
+struct LeafJob {      // 32 B in LDS, one per traversal lane
+    uint32_t state;   // 0 idle, 1 posted, 2 answered
+    uint32_t pos;     // queue position of the ray
+    uint32_t lx, ly;  // leaf slot
+    float t_accept;
+    uint32_t prim;    // answer: kPrimNone = no accepted hit
+    float t;
+    uint32_t flags;   // inside | axis << 1 | neg << 3
+};
+
+__host__ __device__ __forceinline__ size_t split_stack_bytes(uint32_t depth) {
+    return ((size_t)depth * kTravLanes * (sizeof(uint2) + sizeof(uint16_t)) + 15u) & ~(size_t)15u;
+}
+
+template <bool kCuboids>
+__global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
+                                                                 uint32_t unused, unsigned long long *__restrict__ stats) {
+    extern __shared__ uint2 lds_stack[];
+    __shared__ uint32_t live;            // traversal waves still running
+    __shared__ uint32_t worklist[64];    // leaf wave: job indices of one round
+    LeafJob *jobs = reinterpret_cast<LeafJob *>(reinterpret_cast<char *>(lds_stack) + split_stack_bytes(S.depth));
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
+    if (tid < kTravLanes) jobs[tid].state = 0u;
+    if (tid == 0u) live = kTravLanes / 64u;
+    if (blockIdx.x == 0 && tid < kSegs) {  // the other queue is refilled by this iteration's shade
+        B.ctrl[ctr_count(q ^ 1u, tid)] = 0u;
+        B.ctrl[ctr_head(q ^ 1u, tid)] = 0u;
+    }
+    __syncthreads();
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (tid >= kTravLanes) {
+        // ------------------------------------------------------------- leaf wave
+        for (;;) {
+            const bool p0 = __hip_atomic_load(&jobs[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u;
+            const bool p1 = __hip_atomic_load(&jobs[lane + 64u].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u;
+            const bool p2 = __hip_atomic_load(&jobs[lane + 128u].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u;
+            const uint64_t m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2);
+            const uint32_t n0 = (uint32_t)__popcll(m0), n1 = (uint32_t)__popcll(m1), n2 = (uint32_t)__popcll(m2);
+            const uint32_t n = n0 + n1 + n2;
+            if (n == 0u) {
+                if (__hip_atomic_load(&live, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) break;
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            // compact the posted job indices into the work list (first 64 this round)
+            uint32_t r;
+            if (p0 && (r = lanes_below(m0)) < 64u) worklist[r] = lane;
+            if (p1 && (r = n0 + lanes_below(m1)) < 64u) worklist[r] = lane + 64u;
+            if (p2 && (r = n0 + n1 + lanes_below(m2)) < 64u) worklist[r] = lane + 128u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < (n < 64u ? n : 64u)) {
+                const uint32_t j = worklist[lane];
+                const uint32_t pos = jobs[j].pos;
+                const uint2 slot = make_uint2(jobs[j].lx, jobs[j].ly);
+                const float t_accept = jobs[j].t_accept;
+                const float4 r0 = ray0[pos], r1 = ray1[pos];
+                const TraceRay tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
+                                                   (__float_as_uint(r1.w) >> 31) != 0u);
+                uint32_t prim = kPrimNone;
+                PrimHit h;
+                const bool found = leaf_test<kCuboids>(S, tr, slot, t_accept, prim, h, cnt);
+                jobs[j].prim = found ? prim : kPrimNone;
+                jobs[j].t = h.t;
+                jobs[j].flags = h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u);
+                __hip_atomic_store(&jobs[j].state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __builtin_amdgcn_wave_barrier();  // the work list is rewritten next round
+        }
+    } else {
+        // ------------------------------------------------------------- traversal waves
+        const StackT<kTravLanes> stk = stack_of<kTravLanes>(lds_stack, S.depth);
+        uint32_t seg = __builtin_amdgcn_readfirstlane((blockIdx.x * (kTravLanes / 64u) + (tid >> 6)) % kSegs);
+        uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
+        bool rays_left = true;
+        uint32_t segs_w = 0u;
+        bool active = false, pend = false;
+        uint32_t pos = 0u;
+        TraceRay tr;
+        Esvo E;
+        uint2 leaf = make_uint2(0u, 0u);
+        float t_accept = 0.0f;
+        for (;;) {
+            const bool idle = !active;
+            const uint64_t im = __ballot(idle);
+            if (rays_left && im != 0ull && ((uint32_t)__popcll(im) >= refill || ~im == 0ull)) {
+                const uint32_t my = wave_ticket(B.ctrl + ctr_head(q, seg), idle);
+                bool dry = false;
+                if (idle) {
+                    if (my < seg_n) {
+                        pos = seg * B.seg_cap + my;
+                        const float4 r0 = ray0[pos], r1 = ray1[pos];
+                        tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
+                                            (__float_as_uint(r1.w) >> 31) != 0u);
+                        esvo_begin(S, tr, E, stk);
+                        active = true;
+                    } else {
+                        dry = true;
+                    }
+                }
+                segs_w += (uint32_t)__popcll(__ballot(idle && !dry));
+                if (__ballot(dry) != 0ull) {
+                    const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, lane)) < B.ctrl[ctr_count(q, lane)]);
+                    rays_left = m != 0ull;
+                    if (rays_left) {
+                        seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
+                        seg_n = B.ctrl[ctr_count(q, seg)];
+                    }
+                }
+            }
+            const uint64_t am = __ballot(active);
+            if (am == 0ull && !rays_left) break;
+            if (pend) {  // answered leaf test?
+                if (__hip_atomic_load(&jobs[tid].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
+                    pend = false;
+                    const uint32_t prim = jobs[tid].prim;
+                    const float t = jobs[tid].t;
+                    const uint32_t flags = jobs[tid].flags;
+                    jobs[tid].state = 0u;
+                    if (prim != kPrimNone) {
+                        B.hit[pos] = make_uint4(prim, __float_as_uint(t), flags, 0u);
+                        cnt.steps += E.iter;
+                        active = false;
+                    }
+                }
+            }
+            if (active && !pend) {
+                uint32_t prim = kPrimNone;
+                PrimHit h;
+                const int rs = esvo_step<true, kCuboids>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
+                if (rs == kStepLeaf) {
+                    jobs[tid].pos = pos;
+                    jobs[tid].lx = leaf.x;
+                    jobs[tid].ly = leaf.y;
+                    jobs[tid].t_accept = t_accept;
+                    __hip_atomic_store(&jobs[tid].state, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pend = true;
+                } else if (rs != kStepContinue) {  // kStepMiss (hits come from the leaf wave)
+                    B.hit[pos] = make_uint4(kPrimNone, 0u, 0u, 0u);
+                    cnt.steps += E.iter;
+                    active = false;
+                }
+            }
+            if (__ballot(active && !pend) == 0ull && __ballot(pend) != 0ull) __builtin_amdgcn_s_sleep(1);
+        }
+        cnt.segs = lane == 0u ? segs_w : 0u;
+        if (lane == 0u) __hip_atomic_fetch_add(&live, (uint32_t)-1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    flush_counters(cnt, stats);
+}
+
 // shade: one lane per traced ray (grid-stride, wave-uniform trip count)
 #ifndef OCTPT_SHADE_WAVES
 #define OCTPT_SHADE_WAVES 1
@@ -1359,8 +1528,12 @@ int render_blocks_per_cu(uint32_t depth) {
     return blocks > 0 ? blocks : 1;
 }
 
-// the extend instance a scene / leaf-batch setting launches (sphere-only scenes: no slab test)
+// the extend instance a scene / setting launches (sphere-only scenes: no slab test).
+// leaf_batch: 0 inline leaf tests, 1..64 wave-local deferral, kLeafSplit the wave-specialised kernel
 static const void *extend_instance(const DevScene &S, uint32_t leaf_batch) {
+    if (leaf_batch == kLeafSplit)
+        return S.has_cuboids ? reinterpret_cast<const void *>(wf_extend_split_kernel<true>)
+                             : reinterpret_cast<const void *>(wf_extend_split_kernel<false>);
     if (S.has_cuboids)
         return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, true>)
                           : reinterpret_cast<const void *>(wf_extend_kernel<false, true>);
@@ -1368,10 +1541,15 @@ static const void *extend_instance(const DevScene &S, uint32_t leaf_batch) {
                       : reinterpret_cast<const void *>(wf_extend_kernel<false, false>);
 }
 
+static size_t extend_lds_bytes(const DevScene &S, uint32_t leaf_batch) {
+    return leaf_batch == kLeafSplit ? split_stack_bytes(S.depth) + kTravLanes * sizeof(LeafJob)
+                                    : render_lds_bytes(S.depth);
+}
+
 int extend_blocks_per_cu(const DevScene &S, uint32_t leaf_batch) {
     int blocks = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S, leaf_batch), kBlock,
-                                                     render_lds_bytes(S.depth)) != hipSuccess)
+                                                     extend_lds_bytes(S, leaf_batch)) != hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
 }
@@ -1395,7 +1573,7 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
     // leaf_batch 0: test leaves inside the step (no deferral)
     void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &leaf_batch, &stats};
     const hipError_t e = hipLaunchKernel(extend_instance(S, leaf_batch), dim3(grid), dim3(kBlock), args,
-                                         render_lds_bytes(S.depth), stream);
+                                         extend_lds_bytes(S, leaf_batch), stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

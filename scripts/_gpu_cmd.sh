@@ -1,8 +1,6 @@
 set -o pipefail
-timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+OCTPT_EXTEND=split timeout -k 10 240 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
 tail -1 gpurun_out/t.log
-echo "== C4"; timeout -k 10 200 python scripts/spp_sweep.py C4 16 --ktime 2>&1 | grep spp || exit 1
-for v in base sh5 sh6; do
-  L=""; [ $v != base ] && L=build_variants/$v/liboctpt.so
-  echo "== C3 $v"; OCTPT_LIB=$L timeout -k 10 120 python scripts/spp_sweep.py C3 64 64 --ktime 2>&1 | grep spp || exit 1
-done
+echo "== C3 base"; timeout -k 10 120 python scripts/spp_sweep.py C3 64 64 --ktime 2>&1 | grep spp || exit 1
+echo "== C3 split"; OCTPT_EXTEND=split timeout -k 10 120 python scripts/spp_sweep.py C3 64 64 --ktime 2>&1 | grep spp || exit 1
+echo "== C4 split"; OCTPT_EXTEND=split timeout -k 10 120 python scripts/spp_sweep.py C4 16 --ktime 2>&1 | grep spp || exit 1

@@ -391,3 +391,27 @@ def test_intersect_matches_golden_rays(renderer):
     t, prim, nrm, steps = renderer.intersect(g["rays"])
     assert np.array_equal(prim, g["prim"]) and np.array_equal(steps, g["steps"])
     assert np.array_equal(t, g["t"]) and np.array_equal(nrm, g["normal"])
+
+
+@pytest.mark.parametrize("name,res", [("tiny", None), ("C3", (256, 144, 4)), ("C4", (96, 54, 2))])
+def test_split_extend_equals_default(torch_cuda, renderer, name, res):
+    """The wave-specialised extend kernel (OCTPT_EXTEND=split: 3 traversal waves + 1 leaf-test wave
+    per block) renders bit-identically to the default extend kernel."""
+    import os
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    sc, cam, rs = S.make_config(name)
+    if res:
+        rs.width, rs.height, rs.spp = res
+    ref = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    os.environ["OCTPT_EXTEND"] = "split"
+    try:
+        r2 = HipRenderer(0)
+        out = gpu_render(torch_cuda, r2, sc, cam, rs)
+        r2.close()
+    finally:
+        del os.environ["OCTPT_EXTEND"]
+    assert np.array_equal(ref[0], out[0]) and np.array_equal(ref[1], out[1])
+    for k in ("segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events", "paths"):
+        assert ref[2][k] == out[2][k], k
