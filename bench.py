@@ -37,17 +37,17 @@ METRIC = "Mrays/sec at 1920×1080×256spp; achieved HBM GB/s vs roofline at 1/2/
 
 def extend_bytes(st: dict) -> float:
     """DESIGN.md §8, wf_extend_kernel: 8 B per ESVO iteration (one packed child slot), 16 + 4 B per
-    sphere test (centre/radius float4 + leaf prim index), 32 + 4 B per cuboid test (min/max
-    float4s + index), 48 B per segment (32-B ray record read + 16-B hit record write)."""
-    return (8.0 * st["esvo_steps"] + 20.0 * st["sphere_tests"] + 36.0 * st["cuboid_tests"]
-            + 48.0 * st["segments"])
+    sphere test (centre/radius float4 + leaf prim index), 24 + 4 B per cuboid test (min/max
+    float4 + float2 + index), 40 B per segment (32-B ray record read + 8-B hit record write)."""
+    return (8.0 * st["esvo_steps"] + 20.0 * st["sphere_tests"] + 28.0 * st["cuboid_tests"]
+            + 40.0 * st["segments"])
 
 
 def shade_bytes(st: dict) -> float:
-    """DESIGN.md §8, wf_shade_kernel per segment: ray record 32 + hit 16 + path state 40 read,
+    """DESIGN.md §8, wf_shade_kernel per segment: ray record 32 + hit 8 + path state 40 read,
     path state 40 + ray record 32 written; per shaded hit 16 (sphere) + 4 (material id) + 48
     (material record); 4 B per texel; 16 B per finished path (colour record)."""
-    return (160.0 * st["segments"] + 68.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
+    return (152.0 * st["segments"] + 68.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
 
 
 def load_traffic(config: str):

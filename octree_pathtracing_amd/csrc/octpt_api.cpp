@@ -249,6 +249,8 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d) {
     if (d->leaf_table_size && (!d->leaf_first || !d->leaf_count))
         return fail(ctx, OCTPT_ERR_INVALID_ARG, "leaf table pointers are NULL");
     if (d->leaf_prim_count && !d->leaf_prims) return fail(ctx, OCTPT_ERR_INVALID_ARG, "leaf_prims is NULL");
+    if (d->sphere_count > kPrimIndexMask || d->cuboid_count > kPrimIndexMask)
+        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^27 - 1 spheres or cuboids");
     if (d->sphere_count && !d->spheres) return fail(ctx, OCTPT_ERR_INVALID_ARG, "spheres is NULL");
     if (d->cuboid_count && !d->cuboids) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboids is NULL");
     if (d->sun.sun_sampling)

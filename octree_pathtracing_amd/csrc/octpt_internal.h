@@ -8,6 +8,7 @@ namespace octpt {
 
 constexpr uint32_t kPrimNone = 0xFFFFFFFFu;
 constexpr uint32_t kPrimCuboidBit = 0x80000000u;
+constexpr uint32_t kPrimIndexMask = 0x07FFFFFFu;  // primitive indices < 2^27 (hit records pack flags above)
 constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primary rays
 constexpr uint32_t kBlock = 256;       // threads per block (4 waves)
 constexpr uint32_t kMaxDepth = 21;     // new_octree.rs:14
@@ -107,7 +108,7 @@ struct WaveBuffers {
     float4 *pa;     // (T.xyz, L.x)
     float4 *pb;     // (L.y, L.z, rng, item)
     uint2 *pc;      // (cur_mat, depth | specular << 8 | path_segs << 16)
-    uint4 *hit;     // per queue position: (prim, t, inside | axis << 1 | neg << 3, -)
+    uint2 *hit;     // per queue position: (cuboid bit | flags << 27 | prim index, t) -- hit_record()
     float4 *color;  // per chunk item: (L.xyz, path segments)
     uint32_t *ctrl;    // kCtrlWords sharded counters (see above)
     uint32_t seg_cap;  // positions per queue segment (multiple of 64)

@@ -243,6 +243,13 @@ struct PrimHit {
     float nsgn;
 };
 
+// 8-B hit record (extend -> shade): x = cuboid bit | (inside | axis << 1 | neg << 3) << 27 | prim index
+// (indices < 2^27, validated at upload, so a hit never encodes to kPrimNone), y = t bits
+__device__ __forceinline__ uint2 hit_record(uint32_t prim, const PrimHit &h) {
+    const uint32_t flags = (h.inside & 1u) | ((h.axis & 3u) << 1) | (h.nsgn < 0.0f ? 8u : 0u);
+    return make_uint2((prim & kPrimCuboidBit) | (flags << 27) | (prim & kPrimIndexMask), __float_as_uint(h.t));
+}
+
 // Sphere::hit restated (sphere.rs:33-57) + root selection [C2].  Straight-line: the near root is
 // computed for every lane (the common case), the far root only for lanes that need it (origin
 // inside the sphere, or re-entering the primitive the ray left).
@@ -264,6 +271,8 @@ __device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool s
     }
     h.t = near_ok ? t0 : t1;
     h.inside = near_ok ? 0u : 1u;
+    h.axis = 0u;  // face fields: cuboids only
+    h.nsgn = 1.0f;
     return near_ok || far_ok;
 }
 
@@ -1183,8 +1192,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
                 uint32_t prim = kPrimNone;
                 PrimHit h;
                 if (leaf_test<kCuboids>(S, tr, leaf, t_accept, prim, h, cnt)) {
-                    B.hit[pos] = make_uint4(prim, __float_as_uint(h.t),
-                                            h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u), 0u);
+                    B.hit[pos] = hit_record(prim, h);
                     cnt.steps += E.iter;
                     active = false;
                 }
@@ -1197,11 +1205,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
             if (rs == kStepLeaf) {
                 pend = true;
             } else if (rs != kStepContinue) {
-                uint4 rec = make_uint4(kPrimNone, 0u, 0u, 0u);
-                if (rs == kStepHit)
-                    rec = make_uint4(prim, __float_as_uint(h.t),
-                                     h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u), 0u);
-                B.hit[pos] = rec;
+                B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
                 cnt.steps += E.iter;
                 active = false;
             }
@@ -1286,7 +1290,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
                 const bool found = leaf_test<kCuboids>(S, tr, slot, t_accept, prim, h, cnt);
                 jobs[j].prim = found ? prim : kPrimNone;
                 jobs[j].t = h.t;
-                jobs[j].flags = h.inside | (h.axis << 1) | (h.nsgn < 0.0f ? 8u : 0u);
+                jobs[j].flags = (h.inside & 1u) | ((h.axis & 3u) << 1) | (h.nsgn < 0.0f ? 8u : 0u);
                 __hip_atomic_store(&jobs[j].state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             __builtin_amdgcn_wave_barrier();  // the work list is rewritten next round
@@ -1342,7 +1346,8 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
                     const uint32_t flags = jobs[tid].flags;
                     jobs[tid].state = 0u;
                     if (prim != kPrimNone) {
-                        B.hit[pos] = make_uint4(prim, __float_as_uint(t), flags, 0u);
+                        B.hit[pos] = make_uint2((prim & kPrimCuboidBit) | (flags << 27) | (prim & kPrimIndexMask),
+                                                __float_as_uint(t));
                         cnt.steps += E.iter;
                         active = false;
                     }
@@ -1360,7 +1365,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
                     __hip_atomic_store(&jobs[tid].state, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     pend = true;
                 } else if (rs != kStepContinue) {  // kStepMiss (hits come from the leaf wave)
-                    B.hit[pos] = make_uint4(kPrimNone, 0u, 0u, 0u);
+                    B.hit[pos] = make_uint2(kPrimNone, 0u);
                     cnt.steps += E.iter;
                     active = false;
                 }
@@ -1400,16 +1405,17 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
             const float4 r0 = B.ray0[q][i], r1 = B.ray1[q][i];
             slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
             load_path(B, slot, r0, r1, ps, item);
-            const uint4 hr = B.hit[i];
+            const uint2 hr = B.hit[i];
             const bool hit = hr.x != kPrimNone;
             if (hit) {
                 PrimHit h;
+                const uint32_t flags = (hr.x >> 27) & 15u;
                 h.t = __uint_as_float(hr.y);
-                h.inside = hr.z & 1u;
-                h.axis = (hr.z >> 1) & 3u;
-                h.nsgn = (hr.z & 8u) ? -1.0f : 1.0f;
+                h.inside = flags & 1u;
+                h.axis = (flags >> 1) & 3u;
+                h.nsgn = (flags & 8u) ? -1.0f : 1.0f;
                 ps.n = V(0.0f, 0.0f, 0.0f);
-                commit_hit(S, ps, hr.x, h, cnt);
+                commit_hit(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
             }
             bool cont = shade_segment(S, R, ps, hit, cnt);
             if (cont) cont = begin_segment(ps);
