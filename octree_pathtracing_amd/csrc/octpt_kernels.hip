@@ -236,18 +236,20 @@ __device__ inline void texture_image_value(const DevScene &S, uint32_t tex_idx, 
     out[3] = (float)(px >> 24) / 255.0f;
 }
 
+// a primitive hit: t and the packed face flags inside | axis << 1 | (normal sign < 0) << 3
+// (axis and sign describe the cuboid face; spheres leave them 0)
 struct PrimHit {
     float t;
-    uint32_t inside;
-    uint32_t axis;
-    float nsgn;
+    uint32_t f;
+    __device__ uint32_t inside() const { return f & 1u; }
+    __device__ uint32_t axis() const { return (f >> 1) & 3u; }
+    __device__ float nsgn() const { return (f & 8u) ? -1.0f : 1.0f; }
 };
 
 // 8-B hit record (extend -> shade): x = cuboid bit | (inside | axis << 1 | neg << 3) << 27 | prim index
 // (indices < 2^27, validated at upload, so a hit never encodes to kPrimNone), y = t bits
 __device__ __forceinline__ uint2 hit_record(uint32_t prim, const PrimHit &h) {
-    const uint32_t flags = (h.inside & 1u) | ((h.axis & 3u) << 1) | (h.nsgn < 0.0f ? 8u : 0u);
-    return make_uint2((prim & kPrimCuboidBit) | (flags << 27) | (prim & kPrimIndexMask), __float_as_uint(h.t));
+    return make_uint2((prim & kPrimCuboidBit) | ((h.f & 15u) << 27) | (prim & kPrimIndexMask), __float_as_uint(h.t));
 }
 
 // Sphere::hit restated (sphere.rs:33-57) + root selection [C2].  Straight-line: the near root is
@@ -270,9 +272,7 @@ __device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool s
         far_ok = t1 > RAY_EPSILON;
     }
     h.t = near_ok ? t0 : t1;
-    h.inside = near_ok ? 0u : 1u;
-    h.axis = 0u;  // face fields: cuboids only
-    h.nsgn = 1.0f;
+    h.f = near_ok ? 0u : 1u;
     return near_ok || far_ok;
 }
 
@@ -311,10 +311,9 @@ __device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const Trac
     if (!inside) axis = (mins.x == t0) ? 0u : ((mins.y == t0) ? 1u : 2u);
     else axis = (maxs.x == t1) ? 0u : ((maxs.y == t1) ? 1u : 2u);
     const float ia = axis == 0u ? inv.x : (axis == 1u ? inv.y : inv.z);
-    h.nsgn = inside ? (ia > 0.0f ? 1.0f : -1.0f) : (ia > 0.0f ? -1.0f : 1.0f);
+    const bool neg = inside ? !(ia > 0.0f) : (ia > 0.0f);  // normal sign per intersects_new's face
     h.t = t;
-    h.inside = inside;
-    h.axis = axis;
+    h.f = inside | (axis << 1) | (neg ? 8u : 0u);
     return true;
 }
 
@@ -342,12 +341,14 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
         const float2 cb = S.cub_b[ci];
         const float4 bmin = make_float4(ca.x, ca.y, ca.z, 0.0f), bmax = make_float4(ca.w, cb.x, cb.y, 0.0f);
         n = V(0.0f, 0.0f, 0.0f);
-        if (h.axis == 0u) n.x = h.nsgn; else if (h.axis == 1u) n.y = h.nsgn; else n.z = h.nsgn;
+        const uint32_t axis = h.axis();
+        const float nsgn = h.nsgn();
+        if (axis == 0u) n.x = nsgn; else if (axis == 1u) n.y = nsgn; else n.z = nsgn;
         const float ex = bmax.x - bmin.x, ey = bmax.y - bmin.y, ez = bmax.z - bmin.z;
-        if (h.axis == 0u) {
+        if (axis == 0u) {
             u = (p.z - bmin.z) / ez; v = (p.y - bmin.y) / ey;
             if (r.d.x < 0.0f) u = 1.0f - u;
-        } else if (h.axis == 1u) {
+        } else if (axis == 1u) {
             u = (p.x - bmin.x) / ex; v = (p.z - bmin.z) / ez;
             if (r.d.y < 0.0f) v = 1.0f - v;
         } else {
@@ -356,13 +357,13 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
         }
         u = fabsf(u);
         v = fabsf(v);
-        mat = S.cub_mat[6u * ci + face_index(h.axis, h.nsgn)];
+        mat = S.cub_mat[6u * ci + face_index(axis, nsgn)];
         uv_ready = true;
     }
     r.o = p;
     r.n = n;
     r.last_prim = prim;
-    if (h.inside) {
+    if (h.inside()) {
         r.cur = 0u;
         r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;
     } else {
@@ -1290,7 +1291,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
                 const bool found = leaf_test<kCuboids>(S, tr, slot, t_accept, prim, h, cnt);
                 jobs[j].prim = found ? prim : kPrimNone;
                 jobs[j].t = h.t;
-                jobs[j].flags = (h.inside & 1u) | ((h.axis & 3u) << 1) | (h.nsgn < 0.0f ? 8u : 0u);
+                jobs[j].flags = h.f & 15u;
                 __hip_atomic_store(&jobs[j].state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             __builtin_amdgcn_wave_barrier();  // the work list is rewritten next round
@@ -1411,9 +1412,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
                 PrimHit h;
                 const uint32_t flags = (hr.x >> 27) & 15u;
                 h.t = __uint_as_float(hr.y);
-                h.inside = flags & 1u;
-                h.axis = (flags >> 1) & 3u;
-                h.nsgn = (flags & 8u) ? -1.0f : 1.0f;
+                h.f = flags;
                 ps.n = V(0.0f, 0.0f, 0.0f);
                 commit_hit(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
             }
