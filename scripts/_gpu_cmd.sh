@@ -1,5 +1,4 @@
 set -o pipefail
 timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
 tail -1 gpurun_out/t.log
-echo "== C4"; timeout -k 10 200 python scripts/spp_sweep.py C4 16 --ktime 2>&1 | grep spp || exit 1
-echo "== C3"; timeout -k 10 120 python scripts/spp_sweep.py C3 64 64 --ktime 2>&1 | grep spp || exit 1
+echo "== C3"; timeout -k 10 120 python scripts/spp_sweep.py C3 256 --ktime 2>&1 | grep spp || exit 1
