@@ -447,6 +447,9 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_cuboids ? 1 : 0][ctx->leaf_batch == kLeafSplit ? 2 : (ctx->leaf_batch ? 1 : 0)];
     if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S, ctx->leaf_batch);
     const int grid_extend = ctx->num_cu * bpc;
+    if (std::getenv("OCTPT_DEBUG"))
+        std::fprintf(stderr, "octpt: extend %d blocks/CU x %d CUs (depth %u, cuboids %u, variant %u), pool %zu\n", bpc,
+                     ctx->num_cu, ctx->S.depth, ctx->S.has_cuboids, ctx->leaf_batch, pool);
     // shade maps waves to queue segments: a multiple of kSegs waves (kSegs / 4 blocks)
     const int seg_blocks = (int)(kSegs * 64u / kBlock);
     const int grid_shade = (ctx->num_cu * 4 + seg_blocks - 1) / seg_blocks * seg_blocks;

@@ -399,7 +399,7 @@ template <uint32_t kS = kBlock>
 __device__ __forceinline__ StackT<kS> stack_of(uint2 *lds, uint32_t depth) {
     StackT<kS> s;
     s.e = lds + threadIdx.x;
-    s.m = reinterpret_cast<uint16_t *>(lds + (size_t)depth * kS) + threadIdx.x;
+    s.m = reinterpret_cast<uint16_t *>(lds + (size_t)(depth - 1u) * kS) + threadIdx.x;
     return s;
 }
 
@@ -558,9 +558,11 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     if (cz) E.pos.z = E.pos.z + delta;
     const uint32_t step_mask = (cx ? 1u : 0u) | (cy ? 2u : 0u) | (cz ? 4u : 0u);
     if (descend) {
-        // validated trees never descend below the leaf level, so the slot is in [0, depth)
-        // stack slot = scale - (OCTREE_MAX_SCALE - depth) = exponent(scale_exp2) - 127 + depth
-        const int slot_i = (int)(__float_as_uint(E.scale_exp2) >> 23) - 127 + (int)S.depth;
+        // level = scale - (OCTREE_MAX_SCALE - depth) = exponent(scale_exp2) - 127 + depth is in
+        // [1, depth): leaf cells (level 0) are never descended from, and a pop always rises at least
+        // one level above them, so level 0 is never written or read and LDS holds levels 1..depth-1
+        // (stack slot = level - 1; the oracle's level-0 entry stays zero, like the miss below)
+        const int slot_i = (int)(__float_as_uint(E.scale_exp2) >> 23) - 128 + (int)S.depth;
         if (tc_max < E.h && slot_i >= 0) stk_write(stk, (uint32_t)slot_i, E.parent, E.t_max, E.pmask);
     }
     E.h = descend ? tc_max : E.h;
@@ -582,9 +584,9 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const uint32_t base = OCTREE_MAX_SCALE - S.depth;
         uint2 e = make_uint2(0u, 0u);
         uint32_t em = S.node0_mask;
-        if (scale >= base) {
-            e = stk.e[(scale - base) * kS];
-            em = stk.m[(scale - base) * kS];
+        if (scale > base) {
+            e = stk.e[(scale - base - 1u) * kS];
+            em = stk.m[(scale - base - 1u) * kS];
         }
         E.parent = e.x;
         E.pmask = em;
@@ -1236,7 +1238,7 @@ struct LeafJob {      // 32 B in LDS, one per traversal lane
 };
 
 __host__ __device__ __forceinline__ size_t split_stack_bytes(uint32_t depth) {
-    return ((size_t)depth * kTravLanes * (sizeof(uint2) + sizeof(uint16_t)) + 15u) & ~(size_t)15u;
+    return ((size_t)(depth - 1u) * kTravLanes * (sizeof(uint2) + sizeof(uint16_t)) + 15u) & ~(size_t)15u;
 }
 
 template <bool kCuboids>
@@ -1523,7 +1525,8 @@ __global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t N, const float4 
 
 }  // namespace
 
-size_t render_lds_bytes(uint32_t depth) { return (size_t)depth * kBlock * (sizeof(uint2) + sizeof(uint16_t)); }
+// ESVO stack levels 1..depth-1 (level 0 is never used, see esvo_step)
+size_t render_lds_bytes(uint32_t depth) { return (size_t)(depth - 1u) * kBlock * (sizeof(uint2) + sizeof(uint16_t)); }
 
 int render_blocks_per_cu(uint32_t depth) {
     int blocks = 0;
