@@ -134,6 +134,10 @@ typedef struct octpt_camera {
 #define OCTPT_RENDER_SHARD_COMPACT 0x1u /* accum holds only this shard's 8x8 tiles, tile-major */
 #define OCTPT_RENDER_MEGAKERNEL 0x2u    /* single persistent megakernel instead of the wavefront loop (A/B) */
 #define OCTPT_RENDER_KERNEL_TIMING 0x4u /* bracket every extend / shade launch with HIP events (octpt_stats) */
+/* RendererMode::Preview (tile_renderer.rs:293, render_tile_replace :648-682; preview_render,
+ * path_tracer.rs:137-158): one un-jittered camera ray per pixel, flat-shaded by the sun
+ * (Sun::flat_shading, scene/mod.rs:447-452); rgb is replaced, alpha kept; spp/max_depth ignored */
+#define OCTPT_RENDER_PREVIEW 0x8u
 typedef struct octpt_render_params {
     uint32_t width, height;
     uint32_t spp_start, spp_count;

@@ -29,6 +29,7 @@ TEXTURE_IMAGE = 1
 RENDER_SHARD_COMPACT = 0x1
 RENDER_MEGAKERNEL = 0x2
 RENDER_KERNEL_TIMING = 0x4
+RENDER_PREVIEW = 0x8
 PRIM_NONE = 0xFFFFFFFF
 PRIM_CUBOID_BIT = 0x80000000
 

@@ -178,6 +178,7 @@ void make_sun(const octpt_sun &p, const float lut_float[256], DevSun &k) {
         const float atb = (p.texture_modification ? p.apparent_color[i] : 1.0f) * gamma_b;
         k.isect_mul[i] = atb * 10.0f;
         k.diffuse_mul[i] = p.color[i] * 10.0f;
+        k.emit[i] = p.color[i] * gamma_b;
     }
     k.luminosity = p.luminosity;
     const float pi = 3.14159265358979323846f;
@@ -333,6 +334,9 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     R.shard_tiles = tiles_of_shard(R.tiles_x * tiles_y, p->shard_index, p->shard_count);
     R.total_items = R.shard_tiles * 64u;
     R.dim = (float)std::max(p->width, p->height);
+    // RendererMode::Preview renders one replacing pass; spp and max_depth do not apply (C16)
+    R.preview = (p->flags & OCTPT_RENDER_PREVIEW) ? 1u : 0u;
+    if (R.preview) R.spp_count = 1u;
     return OCTPT_OK;
 }
 
@@ -503,8 +507,14 @@ octpt_status enqueue_render(octpt_ctx *ctx, const DevRender &R, float4 *d_accum,
     HIP_TRY(ctx, hipEventCreate(&ev.stop));
     ctx->pending.push_back(ev);  // destroyed by get_stats / destroy
     HIP_TRY(ctx, hipEventRecord(ev.start, s));
-    octpt_status st = megakernel ? enqueue_megakernel(ctx, R, d_accum, d_seg, s)
-                                 : enqueue_wavefront(ctx, R, d_accum, d_seg, s, cancel);
+    octpt_status st = OCTPT_OK;
+    if (R.preview) {
+        const hipError_t e = launch_preview(ctx->S, ctx->C, R, d_accum, d_seg, ctx->d_stats, s);
+        if (e != hipSuccess) st = hip_fail(ctx, e, "preview launch");
+    } else {
+        st = megakernel ? enqueue_megakernel(ctx, R, d_accum, d_seg, s)
+                        : enqueue_wavefront(ctx, R, d_accum, d_seg, s, cancel);
+    }
     HIP_TRY(ctx, hipEventRecord(ev.stop, s));
     if (st == OCTPT_OK) ctx->launches++;
     return st;

@@ -40,6 +40,7 @@ struct DevSun {
     float tex[4];
     float isect_mul[3];
     float diffuse_mul[3];
+    float emit[3];  // Sun::emmittance = color * INTENSITY^GAMMA (scene/mod.rs:352-353), preview shading
     float luminosity;
     float sun_dx, sun_dy, sun_dz;
     float circle_radius, sample_chance;
@@ -85,6 +86,7 @@ struct DevRender {
     uint32_t shard_tiles;    // tiles owned by this shard
     uint32_t total_items;    // shard_tiles * 64 work items
     float dim;               // max(W, H)
+    uint32_t preview;        // RendererMode::Preview
 };
 
 // wavefront path tracer state.
@@ -134,6 +136,8 @@ constexpr uint32_t kStatWords = kSegs * kStatRow;
 constexpr uint32_t kLeafSplit = 0xFFFFu;
 
 // kernel launchers (octpt_kernels.hip)
+hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
+                          uint32_t *segcount, unsigned long long *stats, hipStream_t stream);
 hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
                          uint32_t *segcount, uint32_t *counter, unsigned long long *stats, int grid,
                          hipStream_t stream);

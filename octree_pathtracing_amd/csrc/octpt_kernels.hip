@@ -1009,6 +1009,82 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
 }
 
 // ===========================================================================
+// RendererMode::Preview: render_tile_replace (tile_renderer.rs:648-682) +
+// preview_render (path_tracer.rs:137-158).  One un-jittered camera ray per pixel, continued
+// through material-0 and transparent hits (next_intersection_preview, :447-455), then sky + sun on
+// material 0 or Sun::flat_shading (scene/mod.rs:447-452).  Coherent primary rays: one thread per
+// pixel in 8x8 tiles (one tile per wave), no queues.
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void preview_kernel(DevScene S, DevCamera C, DevRender R,
+                                                         float4 *__restrict__ accum, uint32_t *__restrict__ segcount,
+                                                         unsigned long long *__restrict__ stats) {
+    extern __shared__ uint2 lds_stack[];
+    const Stack stk = stack_of(lds_stack, S.depth);
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    const uint32_t item = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t x = 0u, y = 0u;
+    if (item < R.total_items) item_pixel(R, item, x, y);
+    if (item < R.total_items && x < R.W && y < R.H) {
+        const uint32_t pix = y * R.W + x;
+        PathState ps;
+        // Camera::get_ray at the pixel centre (camera.rs:77-86), no jitter
+        const float xn = ((float)(2u * x + 1u) - (float)R.W) / R.dim;
+        const float yn = ((float)(2u * (R.H - y) - 1u) - (float)R.H) / R.dim;
+        const v3 nd = vadd(vadd(vscale(V(C.dir[0], C.dir[1], C.dir[2]), C.d_factor),
+                                vscale(V(C.right[0], C.right[1], C.right[2]), xn)),
+                           vscale(V(C.up[0], C.up[1], C.up[2]), yn));
+        ps.o = V(C.eye[0], C.eye[1], C.eye[2]);
+        ps.d = vnorm(nd);
+        ps.n = V(0.0f, 0.0f, 0.0f);
+        ps.col[0] = ps.col[1] = ps.col[2] = ps.col[3] = 0.0f;
+        ps.T = V(1.0f, 1.0f, 1.0f);
+        ps.L = V(0.0f, 0.0f, 0.0f);
+        ps.cur = ps.prev = ps.depth = 0u;
+        ps.rng = 0u;
+        ps.last_prim = kPrimNone;
+        ps.path_segs = 0u;
+        ps.specular = true;
+        cnt.paths++;
+        uint32_t pix_segs = 0u;
+        while (begin_segment(ps)) {  // [C15] bounds the pass-through chain
+            cnt.segs++;
+            pix_segs++;
+            const TraceRay tr = trace_ray_of(S, ps);
+            Esvo E;
+            esvo_begin(S, tr, E, stk);
+            uint32_t prim = kPrimNone;
+            PrimHit h;
+            uint2 lf;
+            float ta;
+            int rs;
+            do {
+                rs = esvo_step<false>(S, tr, E, stk, cnt, prim, h, lf, ta);
+            } while (rs == kStepContinue);
+            cnt.steps += E.iter;
+            if (rs != kStepHit) break;  // a miss leaves the last hit record in place
+            commit_hit(S, ps, prim, h, cnt);
+            if (ps.cur != 0u && ps.col[3] > 0.0f) break;
+            ps.o = vadd(ps.o, vscale(ps.d, RAY_OFFSET));
+        }
+        float out[3];
+        if (ps.cur == 0u) {
+            sky_color(S.sun, ps, out);  // depth 0: get_sky_color_inner + add_sun_color
+        } else {
+            const float shading = fmaxf(0.3f, vdot(ps.n, V(S.sun.sw[0], S.sun.sw[1], S.sun.sw[2])));  // AMBIENT
+            for (int i = 0; i < 3; ++i) out[i] = ps.col[i] * (S.sun.emit[i] * shading);
+        }
+        const uint32_t ai = R.compact ? item : pix;
+        float4 fb = accum[ai];
+        fb.x = out[0];
+        fb.y = out[1];
+        fb.z = out[2];
+        accum[ai] = fb;
+        if (segcount) segcount[ai] += pix_segs;
+    }
+    flush_counters(cnt, stats);
+}
+
+// ===========================================================================
 // wavefront path tracer: seed -> (extend -> shade)* -> resolve
 // ===========================================================================
 // Records (16 bytes each).  Ray records live at their queue position, so extend reads them
@@ -1560,6 +1636,14 @@ int extend_blocks_per_cu(const DevScene &S, uint32_t leaf_batch) {
                                                      extend_lds_bytes(S, leaf_batch)) != hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
+}
+
+hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
+                          uint32_t *segcount, unsigned long long *stats, hipStream_t stream) {
+    const uint32_t grid = (R.total_items + kBlock - 1u) / kBlock;
+    hipLaunchKernelGGL(preview_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R, accum,
+                       segcount, stats);
+    return hipGetLastError();
 }
 
 hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum, uint32_t *segcount,

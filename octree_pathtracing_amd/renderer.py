@@ -149,9 +149,9 @@ class HipRenderer:
         return self._status
 
     def set_mode(self, mode: RendererMode) -> None:
-        if mode is not RendererMode.PathTraced:
-            raise _lib.OctptError(_lib.ERR_UNSUPPORTED, "Preview mode is not implemented on the HIP path yet")
-        self._mode = mode
+        """TileRenderer::set_mode (tile_renderer.rs:188-191): stops and restarts the accumulation."""
+        self._mode = RendererMode(mode)
+        self.reset_render()
 
     def get_mode(self) -> RendererMode:
         return self._mode
@@ -173,8 +173,11 @@ class HipRenderer:
         if self._accum is None:
             self._accum = np.zeros((H, W, 4), np.float32)
             self._accum[..., 3] = 1.0
+        preview = self._mode is RendererMode.Preview
         n = spp_count if spp_count is not None else max(self.target_spp - self._spp, 1)
-        p = self.params(W, H, self._spp, n)
+        if preview:  # render_preview (tile_renderer.rs:339-374): one replacing pass, current_spp stays 0
+            n = 0
+        p = self.params(W, H, self._spp, n, preview=preview)
         rgba = np.zeros((H, W, 4), np.uint8)
         h = C.c_void_p()
         self._check(self._lib.octpt_render_async(self._ctx, C.byref(p), self._accum.ctypes.data_as(C.c_void_p),
@@ -206,9 +209,9 @@ class HipRenderer:
 
     # ------------------------------------------------------------ direct entry points
     def params(self, W, H, spp_start, spp_count, shard_index=0, shard_count=1, compact=False,
-               megakernel=False, kernel_timing=False) -> "_lib.RenderParams":
+               megakernel=False, kernel_timing=False, preview=False) -> "_lib.RenderParams":
         flags = ((_lib.RENDER_SHARD_COMPACT if compact else 0) | (_lib.RENDER_MEGAKERNEL if megakernel else 0)
-                 | (_lib.RENDER_KERNEL_TIMING if kernel_timing else 0))
+                 | (_lib.RENDER_KERNEL_TIMING if kernel_timing else 0) | (_lib.RENDER_PREVIEW if preview else 0))
         return _lib.RenderParams(W, H, spp_start, spp_count, self.max_depth, 1, self.seed, shard_index, shard_count,
                                  flags)
 

@@ -269,6 +269,7 @@ typedef struct {
     float diffuse_mul[3];         /* color * 10 */
     int draw_texture;
     float luminosity;
+    float emit[3];                /* Sun::emmittance = color * INTENSITY^GAMMA (scene/mod.rs:352-353) */
     /* diffuse_reflection importance sampling (ray/mod.rs:227-258) */
     float sun_dx, sun_dy, sun_dz, circle_radius, sample_chance;
     int importance_sampling, diffuse_sun;
@@ -310,6 +311,7 @@ static void sun_init(const ref_sun *p, sun_k *k) {
     for (int i = 0; i < 3; i++) {
         k->isect_mul[i] = atb[i] * 10.0f;
         k->diffuse_mul[i] = p->color[i] * 10.0f;
+        k->emit[i] = p->color[i] * gamma_b;
     }
     k->draw_texture = p->draw_texture;
     k->luminosity = p->luminosity;
@@ -1023,6 +1025,59 @@ typedef struct {
     ref_stats total;
 } job_t;
 
+/* preview_render (path_tracer.rs:137-158) with next_intersection_preview (:447-455) and
+ * Sun::flat_shading (scene/mod.rs:447-452) [C16].  Intersection = Scene::hit [C1]; the loop skips
+ * material-0 and transparent (alpha 0) hits from hit + OFFSET*dir, bounded by [C15].  After a miss
+ * the last hit's material decides the shading, exactly as written (a miss leaves the record). */
+static void preview_pixel(ctx_t *c, ray_t *ray, uint32_t *segs, float col[3]) {
+    ray->cur_mat = 0;
+    for (;;) {
+        if (c->path_segs >= MAX_PATH_SEGMENTS) break; /* [C15] */
+        if (!next_intersection(c, ray, segs)) break;
+        if (ray->cur_mat != 0 && ray->col[3] > 0.0f) break;
+        ray->o = ray_at(ray, RAY_OFFSET);
+    }
+    if (ray->cur_mat == 0) { /* get_sky_color_inner + add_sun_color */
+        sky_set(ray);
+        add_sun_color(&c->sun, ray);
+        for (int i = 0; i < 3; i++) col[i] = ray->col[i];
+    } else {
+        float shading = vdot(ray->n, c->sun.sw);
+        shading = fmaxf(0.3f, shading); /* Sun::AMBIENT.max(shading), scene/mod.rs:318 */
+        for (int i = 0; i < 3; i++) col[i] = ray->col[i] * (c->sun.emit[i] * shading);
+    }
+}
+
+/* RendererMode::Preview: render_tile_replace (tile_renderer.rs:648-682) -- one un-jittered
+ * camera ray per pixel, rgb replaced, alpha untouched */
+static void preview_rows(job_t *j, ctx_t *c) {
+    const ref_render_params *p = j->p;
+    uint32_t W = p->width, H = p->height;
+    float dim = (float)(W > H ? W : H);
+    for (;;) {
+        pthread_mutex_lock(&j->lock);
+        uint32_t y = j->next_row++;
+        pthread_mutex_unlock(&j->lock);
+        if (y >= p->row_end) break;
+        for (uint32_t x = 0; x < W; x++) {
+            uint32_t pix = y * W + x;
+            float *fb = &j->accum[4 * (size_t)pix];
+            uint32_t segs = 0;
+            float xn = ((float)(2 * x + 1) - (float)W) / dim;
+            float yn = ((float)(2 * (H - y) - 1) - (float)H) / dim;
+            v3 nd = vadd(vadd(vscale(j->cdir, j->d_factor), vscale(j->cright, xn)), vscale(j->cup, yn));
+            ray_t ray;
+            ray_new(&ray, j->ceye, vnorm(nd));
+            c->st.paths++;
+            c->path_segs = 0;
+            float col[3];
+            preview_pixel(c, &ray, &segs, col);
+            for (int i = 0; i < 3; i++) fb[i] = col[i];
+            if (j->seg_count) j->seg_count[pix] = segs;
+        }
+    }
+}
+
 static void render_rows(job_t *j, ctx_t *c) {
     const ref_render_params *p = j->p;
     uint32_t W = p->width, H = p->height;
@@ -1078,7 +1133,8 @@ static void *render_worker(void *arg) {
     c.max_depth = j->p->max_depth;
     c.branch_count = j->p->branch_count ? j->p->branch_count : 1;
     c.forward = j->p->forward_accumulation && c.branch_count == 1;
-    render_rows(j, &c);
+    if (j->p->preview) preview_rows(j, &c);
+    else render_rows(j, &c);
     pthread_mutex_lock(&j->lock);
     j->total.paths += c.st.paths;
     j->total.segments += c.st.segments;

@@ -94,6 +94,8 @@ typedef struct {
     int32_t forward_accumulation; /* 0: recursive (reference), 1: forward (kernel order) */
     /* optional pixel subset: rows [row_begin, row_end) */
     uint32_t row_begin, row_end;
+    /* 1: RendererMode::Preview -- render_tile_replace + preview_render */
+    int32_t preview;
 } ref_render_params;
 
 typedef struct {

@@ -58,7 +58,7 @@ class RefParams(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp_start", C.c_uint32), ("spp_count", C.c_uint32),
                 ("max_depth", C.c_uint32), ("branch_count", C.c_uint32), ("seed", C.c_uint32),
                 ("threads", C.c_uint32), ("forward_accumulation", C.c_int32), ("row_begin", C.c_uint32),
-                ("row_end", C.c_uint32)]
+                ("row_end", C.c_uint32), ("preview", C.c_int32)]
 
 
 class RefStats(C.Structure):
@@ -204,8 +204,9 @@ class OracleScene:
 
 
 def render(scene, camera, width, height, spp, *, spp_start=0, max_depth=5, seed=1, threads=8, forward=False,
-           accum=None, rows=None, branch_count=1):
-    """TileRenderer progressive render on the CPU: returns (accum[H,W,4], seg_count[H,W], stats)."""
+           accum=None, rows=None, branch_count=1, preview=False):
+    """TileRenderer progressive render on the CPU: returns (accum[H,W,4], seg_count[H,W], stats).
+    preview=True: RendererMode::Preview (one un-jittered flat-shaded pass, rgb replaced; spp ignored)."""
     lib = load()
     os_ = OracleScene(scene)
     cam = RefCamera((C.c_float * 3)(*camera.eye), (C.c_float * 3)(*camera.direction), (C.c_float * 3)(*camera.up),
@@ -216,7 +217,8 @@ def render(scene, camera, width, height, spp, *, spp_start=0, max_depth=5, seed=
     accum = np.ascontiguousarray(accum, np.float32)
     segs = np.zeros((height, width), np.uint32)
     r0, r1 = rows if rows else (0, height)
-    p = RefParams(width, height, spp_start, spp, max_depth, branch_count, seed, threads, int(forward), r0, r1)
+    p = RefParams(width, height, spp_start, spp, max_depth, branch_count, seed, threads, int(forward), r0, r1,
+                  int(preview))
     st = RefStats()
     rc = lib.ref_render(C.byref(os_.s), C.byref(cam), C.byref(p), _p(accum), _p(segs), C.byref(st))
     if rc != 0:

@@ -5,7 +5,8 @@ The reference itself cannot be built or run here (Rust toolchain absent, nightly
 synthetic inputs.  They pin the oracle against drift (tests/test_golden_cpu.py) and are the
 committed expected outputs of the GPU parity tests (tests/test_gpu_parity.py).
 
-Usage: python tests/golden/make_golden.py   (rewrites the .npz files next to this script)
+Usage: python tests/golden/make_golden.py [NAME ...]   (rewrites all, or the named, .npz files next
+to this script)
 """
 import json
 import sys
@@ -31,6 +32,11 @@ RENDERS = {
     "c3_small": ("C3", 96, 54, 2, None),
     "c4_small": ("C4", 64, 36, 2, None),  # cuboids + image textures (procedural, scene.py)
 }
+# RendererMode::Preview fixtures: name -> (config, width, height)
+PREVIEWS = {
+    "c3_preview": ("C3", 192, 108),
+    "c4_preview": ("C4", 128, 72),  # transparent texels exercise the pass-through loop
+}
 
 
 def render_fixture(name):
@@ -41,6 +47,15 @@ def render_fixture(name):
     return dict(accum=acc, segcount=seg, stats=np.array([st[k] for k in STAT_KEYS], np.uint64),
                 meta=np.array(json.dumps(dict(config=cfg, width=W, height=H, spp=spp,
                                               max_depth=md or rs.max_depth, seed=rs.seed, forward=True))))
+
+
+def preview_fixture(name):
+    cfg, W, H = PREVIEWS[name]
+    sc, cam, rs = S.make_config(cfg)
+    acc, seg, st = cpu_ref.render(sc, cam, W, H, 1, max_depth=rs.max_depth, seed=rs.seed, threads=8, preview=True)
+    return dict(accum=acc, segcount=seg, stats=np.array([st[k] for k in STAT_KEYS], np.uint64),
+                meta=np.array(json.dumps(dict(config=cfg, width=W, height=H, spp=1, max_depth=rs.max_depth,
+                                              seed=rs.seed, forward=True, preview=True))))
 
 
 def ray_fixture():
@@ -60,13 +75,15 @@ def ray_fixture():
     return dict(rays=rays, t=t, prim=prim, normal=nrm, steps=steps)
 
 
-def main():
-    for name in RENDERS:
-        np.savez_compressed(HERE / f"{name}.npz", **render_fixture(name))
+def main(names):
+    makers = {**{n: render_fixture for n in RENDERS}, **{n: preview_fixture for n in PREVIEWS}}
+    for name in names or [*makers, "c3_rays"]:
+        if name == "c3_rays":
+            np.savez_compressed(HERE / "c3_rays.npz", **ray_fixture())
+        else:
+            np.savez_compressed(HERE / f"{name}.npz", **makers[name](name))
         print("wrote", name)
-    np.savez_compressed(HERE / "c3_rays.npz", **ray_fixture())
-    print("wrote c3_rays")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

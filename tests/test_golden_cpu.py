@@ -11,7 +11,7 @@ from oracle import cpu_ref
 from octree_pathtracing_amd import scene as S
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
-RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small"]
+RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c3_preview", "c4_preview"]
 STAT_KEYS = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
              "texel_reads", "max_path_segs")
 
@@ -26,7 +26,7 @@ def test_oracle_reproduces_render_fixture(name):
     m = json.loads(str(g["meta"]))
     sc, cam, _ = S.make_config(m["config"])
     acc, seg, st = cpu_ref.render(sc, cam, m["width"], m["height"], m["spp"], max_depth=m["max_depth"],
-                                  seed=m["seed"], forward=m["forward"], threads=8)
+                                  seed=m["seed"], forward=m["forward"], threads=8, preview=m.get("preview", False))
     assert np.array_equal(seg, g["segcount"])
     assert np.array_equal(acc, g["accum"])
     assert [st[k] for k in STAT_KEYS] == g["stats"].tolist()

@@ -38,7 +38,8 @@ def rel_err(a, b):
     return np.abs(a - b) / np.maximum(np.abs(b), 1e-3)
 
 
-def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), compact=False, megakernel=False):
+def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), compact=False, megakernel=False,
+               preview=False):
     """Device render through octpt_render_device; returns (accum[H,W,4] or compact, seg_count, stats)."""
     from octree_pathtracing_amd.renderer import shard_pixels
 
@@ -54,7 +55,7 @@ def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), com
     else:
         acc = torch.as_tensor(accum.reshape(-1, 4), device="cuda").clone()
     segs = torch.zeros(n, dtype=torch.int32, device="cuda")
-    p = r.params(W, H, spp_start, rs.spp, shard[0], shard[1], compact, megakernel)
+    p = r.params(W, H, spp_start, rs.spp, shard[0], shard[1], compact, megakernel, preview=preview)
     stream = torch.cuda.current_stream().cuda_stream
     r.render_device(p, acc.data_ptr(), segs.data_ptr(), stream)
     torch.cuda.synchronize()
@@ -355,7 +356,8 @@ def test_wavefront_small_pool_many_chunks(torch_cuda, renderer):
 GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
 
 
-@pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small"])
+@pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c3_preview",
+                                  "c4_preview"])
 def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     """GPU render vs the committed oracle fixture (tests/golden/make_golden.py): exact per-pixel
     segment counts and work totals, radiance within REL_TOL_FORWARD."""
@@ -367,7 +369,7 @@ def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     m = json.loads(str(g["meta"]))
     sc, cam, rs = S.make_config(m["config"])
     rs.width, rs.height, rs.spp, rs.max_depth, rs.seed = m["width"], m["height"], m["spp"], m["max_depth"], m["seed"]
-    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs, preview=m.get("preview", False))
     keys = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
             "texel_reads", "max_path_segs")
     ref = dict(zip(keys, g["stats"].tolist()))
@@ -415,3 +417,70 @@ def test_split_extend_equals_default(torch_cuda, renderer, name, res):
     assert np.array_equal(ref[0], out[0]) and np.array_equal(ref[1], out[1])
     for k in ("segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events", "paths"):
         assert ref[2][k] == out[2][k], k
+
+
+# ---------------------------------------------------------------------------- preview mode (C16)
+@pytest.mark.parametrize("name,res", [("tiny", None), ("C1", None), ("C2", (160, 90)), ("C3", (256, 144)),
+                                      ("C4", (160, 90))])
+def test_preview_parity(torch_cuda, renderer, name, res):
+    """RendererMode::Preview (preview_kernel) vs the oracle: segment counts, work totals and the
+    flat-shaded radiance bit-exact; alpha of the incoming buffer untouched."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config(name)
+    if res:
+        rs.width, rs.height = res
+    pre = np.random.default_rng(3).random((rs.height, rs.width, 4), dtype=np.float32)
+    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs, accum=pre, preview=True)
+    racc, rsegs, rst = oracle(sc, cam, rs, accum=pre.copy(), preview=True)
+    assert np.array_equal(segs, rsegs)
+    assert st["paths"] == rst["paths"] == rs.width * rs.height
+    assert st["segments"] == rst["segments"] and st["esvo_steps"] == rst["esvo_steps"]
+    assert st["sphere_tests"] + st["cuboid_tests"] == rst["prim_tests"] and st["shade_events"] == 0
+    assert st["texel_reads"] == rst["texel_reads"]
+    assert np.array_equal(acc, racc), f"{name}: max abs diff {np.abs(acc - racc).max()}"
+    assert np.array_equal(acc[..., 3], pre[..., 3])
+
+
+def test_preview_shards_union_equals_full(torch_cuda, renderer):
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import shard_pixels
+
+    torch = torch_cuda
+    sc, cam, rs = S.make_config("C4")
+    rs.width, rs.height = 70, 45
+    full = gpu_render(torch, renderer, sc, cam, rs, preview=True)[0]
+    N = 3
+    stride = max(shard_pixels(rs.width, rs.height, i, N) for i in range(N))
+    buf = torch.zeros((N * stride, 4), dtype=torch.float32, device="cuda")
+    for i in range(N):
+        a = gpu_render(torch, renderer, sc, cam, rs, shard=(i, N), compact=True, preview=True)[0]
+        buf[i * stride:i * stride + len(a)] = torch.as_tensor(a, device="cuda")
+    frame = torch.zeros((rs.height * rs.width, 4), dtype=torch.float32, device="cuda")
+    renderer.unshard_device(rs.width, rs.height, N, buf.data_ptr(), stride, frame.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().reshape(rs.height, rs.width, 4), full)
+
+
+def test_renderer_preview_mode(renderer):
+    """HipRenderer.set_mode(Preview) + render_frame (TileRenderer::render_preview): one replacing
+    pass, current spp stays 0, the frame equals the oracle's preview."""
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import RendererMode
+    from oracle import cpu_ref
+
+    sc, cam, rs = S.make_config("C4")
+    W, H = 96, 64
+    renderer.set_scene(sc)
+    renderer.set_camera(cam)
+    renderer.set_resolution((W, H))
+    renderer.set_mode(RendererMode.Preview)
+    try:
+        assert renderer.get_mode() is RendererMode.Preview
+        renderer.render_frame().wait_for()
+        assert renderer.get_current_spp() == 0
+        ref = cpu_ref.render(sc, cam, W, H, 1, preview=True)[0]
+        assert np.array_equal(renderer.get_float_image(), ref)
+    finally:
+        renderer.set_mode(RendererMode.PathTraced)

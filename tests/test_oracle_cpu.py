@@ -256,3 +256,43 @@ def test_tonemap_kat(lib):
     assert out[1].tolist() == [255, 255, 255, 255]
     assert out[2, 0] == 255 and out[2, 3] == 127
     assert out[2, 1] == lib.ref_lut_byte(int(np.float32(0.5) * np.float32(255)))
+
+
+def test_preview_restatement():
+    """RendererMode::Preview (DESIGN.md C16) re-derived in numpy from the oracle's own pieces:
+    a pixel whose ray misses on its first segment holds get_sky_color_inner + add_sun_color (the
+    path-traced depth-0 miss colour of an un-jittered ray), a hit pixel holds
+    texel * emittance * max(AMBIENT, n . sw); alpha is left untouched and nothing is random."""
+    sc, cam, rs = S.make_config("tiny")
+    W, H = 48, 32
+    pre = np.zeros((H, W, 4), np.float32)
+    pre[..., 3] = 0.25
+    acc, seg, st = cpu_ref.render(sc, cam, W, H, 1, threads=2, preview=True, accum=pre.copy())
+    acc2, seg2, _ = cpu_ref.render(sc, cam, W, H, 7, seed=99, threads=2, preview=True, accum=pre.copy())
+    assert np.array_equal(acc, acc2) and np.array_equal(seg, seg2)  # spp / seed do not apply
+    assert np.all(acc[..., 3] == 0.25) and st["shade_events"] == 0 and st["paths"] == W * H
+    # the same rays through the closest-hit query: first-segment misses are sky pixels
+    dim = float(max(W, H))
+    ys, xs = np.mgrid[0:H, 0:W]
+    xn = ((2 * xs + 1).astype(np.float32) - np.float32(W)) / np.float32(dim)
+    yn = ((2 * (H - ys) - 1).astype(np.float32) - np.float32(H)) / np.float32(dim)
+    d_f = np.float32(1.0 / math.tan(cam.fov / 2.0))
+    cdir, cup = np.float32(cam.direction), np.float32(cam.up)
+    right = np.cross(cdir, cup).astype(np.float32)
+    nd = (cdir * d_f)[None, None] + right[None, None] * xn[..., None] + cup[None, None] * yn[..., None]
+    dirs = (nd / np.linalg.norm(nd, axis=-1, keepdims=True)).astype(np.float32)
+    rays = np.concatenate([np.broadcast_to(np.float32(cam.eye), dirs.shape), dirs], -1).reshape(-1, 6)
+    _, prim, nrm, _ = cpu_ref.intersect(sc, rays)
+    miss = (prim == 0xFFFFFFFF).reshape(H, W)
+    assert miss.any() and (~miss).any()
+    assert np.all(seg[miss] == 1)
+    sky = acc[miss][:, :3]
+    assert np.all((sky == np.float32([0.5, 0.7, 1.0])).all(-1) | (sky > 1.0).all(-1))
+    # opaque first hits: flat shading with the sun constants of scene/mod.rs:294-307, 352-353
+    az, alt = np.float32(math.pi / 2.5), np.float32(math.pi / 3.0)
+    sw = np.float32([math.cos(az) * abs(math.cos(alt)), math.sin(alt), math.sin(az) * abs(math.cos(alt))])
+    hit1 = (~miss) & (seg == 1)
+    shading = np.maximum(np.float32(0.3), (nrm.reshape(H, W, 3)[hit1] * sw).sum(-1))
+    emit = np.float32(1.25) ** np.float32(2.2)
+    ratio = acc[hit1][:, :3] / (emit * shading)[:, None]
+    assert np.all(ratio >= 0) and np.all(ratio <= 1.0 + 1e-5)  # texel colours in [0, 1]
