@@ -214,6 +214,16 @@ uint32_t octpt_shard_pixels(uint32_t width, uint32_t height, uint32_t shard_inde
 octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *last_prim, const float *last_normal,
                              uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps);
 
+/* Octree::get_traversal_data (octree_traversal.rs:537-714), the beam-start query of
+ * GPURenderer::render_frame (gpu_renderer.rs:579-581 -> CameraUniform.traversal_start_idx/scale,
+ * index/time stack buffers :35-80).  Walks `ray` (origin xyz, direction xyz, world units) from
+ * the root until the first leaf with t_min > 0 and returns the octant it stopped in, its scale
+ * and the descent stacks, indexed by scale and zero where unwritten.  Host-only and stateless:
+ * no context or device; `octants` is borrowed (the same layout as octpt_scene_desc).
+ * max_dst in world units (Scene::hit uses 1024, scene/mod.rs:181). */
+octpt_status octpt_traversal_data(const octpt_octant *octants, uint32_t octant_count, uint32_t root, uint32_t depth,
+                                  const float ray[6], float max_dst, uint32_t *start_octant, uint32_t *scale,
+                                  uint32_t index_stack[24], float time_stack[24]);
 octpt_status octpt_get_stats(const octpt_ctx *ctx, octpt_stats *stats);
 octpt_status octpt_reset_stats(octpt_ctx *ctx);
 

@@ -150,6 +150,7 @@ SIGNATURES = {
     "octpt_unshard_device": (_i32, [_vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp]),
     "octpt_shard_pixels": (_u32, [_u32, _u32, _u32, _u32]),
     "octpt_intersect": (_i32, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp]),
+    "octpt_traversal_data": (_i32, [_vp, _u32, _u32, _u32, _vp, _f, _vp, _vp, _vp, _vp]),
     "octpt_get_stats": (_i32, [_vp, C.POINTER(Stats)]),
     "octpt_reset_stats": (_i32, [_vp]),
     "octpt_build_octree": (_i32, [_vp, _u32, _vp, _u32, _u32, C.POINTER(_vp)]),

@@ -142,6 +142,22 @@ class Octree:
         return Octree(np.zeros(1, np.uint16), np.zeros((1, 8), np.uint32), 0, depth,
                       np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint32))
 
+    def traversal_data(self, ray, max_dst: float = 1024.0, octants=None):
+        """Octree::get_traversal_data (octree_traversal.rs:537-714) through liboctpt's host query:
+        (start octant, scale, index_stack[24], time_stack[24]) for one ray (origin, direction).
+        `octants` may pass a cached octants_struct() to skip its per-call conversion."""
+        lib = _lib.load()
+        arr = octants if octants is not None else self.octants_struct()
+        r = np.ascontiguousarray(ray, F32).reshape(6)
+        start, scale = C.c_uint32(), C.c_uint32()
+        idx = np.zeros(24, np.uint32)
+        ts = np.zeros(24, F32)
+        st = lib.octpt_traversal_data(C.cast(arr, C.c_void_p), self.octant_count, self.root, self.depth,
+                                      r.ctypes.data_as(C.c_void_p), max_dst, C.byref(start), C.byref(scale),
+                                      idx.ctypes.data_as(C.c_void_p), ts.ctypes.data_as(C.c_void_p))
+        _lib.check(lib, None, st)
+        return start.value, scale.value, idx, ts
+
     def octants_struct(self):
         arr = (_lib.Octant * self.octant_count)()
         buf = np.frombuffer(arr, dtype=np.dtype([("m", "<u2"), ("r", "<u2"), ("c", "<u4", (8,))]))

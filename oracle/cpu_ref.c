@@ -1181,6 +1181,95 @@ int ref_render(const ref_scene *s, const ref_camera *cam, const ref_render_param
     return 0;
 }
 
+/* Octree::get_traversal_data (octree_traversal.rs:537-714): ESVO from the root until the first
+ * leaf with t_min > 0 (:623), returning that parent, its scale and the descent stacks (indexed by
+ * scale, zero where unwritten, :552).  max_dst exit (:609) and the escaping pop (:690-692, which
+ * reports the scale before the pop) return the state reached; |rd| after the clamp [C13]. */
+void ref_traversal_data(const ref_scene *s, const float ray[6], float max_dst_w, uint32_t *start, uint32_t *scale_out,
+                        uint32_t index_stack[24], float time_stack[24]) {
+    float octree_scale = ldexpf(1.0f, -(int)s->depth);
+    memset(index_stack, 0, 24 * sizeof(uint32_t));
+    memset(time_stack, 0, 24 * sizeof(float));
+    v3 ro = vadd(vscale(V(ray[0], ray[1], ray[2]), octree_scale), V(1.0f, 1.0f, 1.0f));
+    v3 rd = V(ray[3], ray[4], ray[5]);
+    float max_dst = max_dst_w * octree_scale;
+    uint32_t parent = s->root, scale = OCTREE_MAX_SCALE - 1;
+    float scale_exp2 = 0.5f;
+    for (int i = 0; i < 3; i++) {
+        float di = vget(rd, i);
+        if (fabsf(di) < OCTREE_EPSILON) vset(&rd, i, u2f((f2u(OCTREE_EPSILON) & 0x7FFFFFFFu) | (f2u(di) & 0x80000000u)));
+    }
+    v3 t_coef = V(1.0f / -fabsf(rd.x), 1.0f / -fabsf(rd.y), 1.0f / -fabsf(rd.z));
+    v3 t_bias = vmul(t_coef, ro);
+    uint32_t mirror = 0;
+    for (int i = 0; i < 3; i++)
+        if (vget(rd, i) > 0.0f) {
+            mirror |= 1u << i;
+            vset(&t_bias, i, 3.0f * vget(t_coef, i) - vget(t_bias, i));
+        }
+    float t_min = fmax_(vmax3(vsub(vscale(t_coef, 2.0f), t_bias)), 0.0f);
+    float t_max = vmin3(vsub(t_coef, t_bias));
+    float h = t_max;
+    uint32_t idx = 0;
+    v3 pos = V(1.0f, 1.0f, 1.0f);
+    v3 upper = vsub(vscale(t_coef, 1.5f), t_bias);
+    for (int i = 0; i < 3; i++)
+        if (vget(upper, i) > t_min) { idx ^= 1u << i; vset(&pos, i, 1.5f); }
+    uint32_t out_scale = scale;
+    for (int it = 0; it < OCTREE_MAX_STEPS; it++) {
+        out_scale = scale;
+        if (max_dst >= 0.0f && t_min > max_dst) break;
+        v3 t_corner = vsub(vmul(pos, t_coef), t_bias);
+        float tc_max = vmin3(t_corner);
+        uint32_t cidx = idx ^ mirror;
+        uint16_t mask = s->octant_mask[parent];
+        int present = (mask >> cidx) & 1, is_leaf = (mask >> (cidx + 8)) & 1;
+        if (present && t_min <= t_max) {
+            if (is_leaf && t_min > 0.0f) break;
+            float half = scale_exp2 * 0.5f;
+            v3 t_center = vadd(vscale(t_coef, half), t_corner);
+            float tv_max = fmin_(t_max, tc_max);
+            if (t_min <= tv_max && !is_leaf) {
+                if (tc_max < h) { index_stack[scale] = parent; time_stack[scale] = t_max; }
+                h = tc_max;
+                parent = s->octant_children[8 * (size_t)parent + cidx];
+                scale -= 1;
+                scale_exp2 = half;
+                idx = 0;
+                for (int i = 0; i < 3; i++)
+                    if (vget(t_center, i) > t_min) { idx ^= 1u << i; vset(&pos, i, vget(pos, i) + scale_exp2); }
+                t_max = tv_max;
+                out_scale = scale;
+                continue;
+            }
+        }
+        uint32_t step_mask = 0;
+        for (int i = 0; i < 3; i++)
+            if (vget(t_corner, i) <= tc_max) { step_mask ^= 1u << i; vset(&pos, i, vget(pos, i) - scale_exp2); }
+        t_min = tc_max;
+        idx ^= step_mask;
+        if ((idx & step_mask) != 0) {
+            uint32_t diff = 0;
+            if (step_mask & 1) diff |= f2u(pos.x) ^ f2u(pos.x + scale_exp2);
+            if (step_mask & 2) diff |= f2u(pos.y) ^ f2u(pos.y + scale_exp2);
+            if (step_mask & 4) diff |= f2u(pos.z) ^ f2u(pos.z + scale_exp2);
+            uint32_t old_scale = scale;
+            scale = diff ? 31u - (uint32_t)__builtin_clz(diff) : 0xFFFFFFFFu;
+            if (scale >= OCTREE_MAX_SCALE) { out_scale = old_scale; break; }
+            scale_exp2 = u2f((scale - OCTREE_MAX_SCALE + 127u) << 23);
+            parent = index_stack[scale];
+            t_max = time_stack[scale];
+            uint32_t shx = f2u(pos.x) >> scale, shy = f2u(pos.y) >> scale, shz = f2u(pos.z) >> scale;
+            pos = V(u2f(shx << scale), u2f(shy << scale), u2f(shz << scale));
+            idx = (shx & 1) | ((shy & 1) << 1) | ((shz & 1) << 2);
+            h = 0.0f;
+        }
+        out_scale = scale;
+    }
+    *start = parent;
+    *scale_out = out_scale;
+}
+
 /* closest-hit query (Scene::hit) for tests */
 void ref_intersect(const ref_scene *s, const float *rays, const uint32_t *last_prim, const float *last_normal,
                    uint32_t n, float *out_t, uint32_t *out_prim, float *out_normal, uint32_t *out_steps) {

@@ -146,6 +146,10 @@ void ref_intersect_brute(const ref_scene *s, const float *rays, uint32_t n, floa
 int ref_render(const ref_scene *s, const ref_camera *cam, const ref_render_params *p, float *accum,
                uint32_t *seg_count, ref_stats *stats);
 
+/* Octree::get_traversal_data (octree_traversal.rs:537-714): beam-start octant, scale, stacks */
+void ref_traversal_data(const ref_scene *s, const float ray[6], float max_dst_w, uint32_t *start, uint32_t *scale,
+                        uint32_t index_stack[24], float time_stack[24]);
+
 /* tone map, colors/mod.rs:408-420 (LUT texture.rs:55-62) */
 void ref_tonemap(const float *accum, uint32_t n_pixels, uint8_t *out_rgba8);
 /* LUT_TABLE_FLOAT (texture.rs:51-54) for tests */

@@ -226,6 +226,19 @@ def render(scene, camera, width, height, spp, *, spp_start=0, max_depth=5, seed=
     return accum, segs, st.as_dict()
 
 
+def traversal_data(scene, ray, max_dst=1024.0):
+    """Octree::get_traversal_data: (start octant, scale, index_stack[24], time_stack[24])."""
+    lib = load()
+    os_ = OracleScene(scene)
+    r = np.ascontiguousarray(ray, np.float32).reshape(6)
+    start, scale = C.c_uint32(), C.c_uint32()
+    idx = np.zeros(24, np.uint32)
+    ts = np.zeros(24, np.float32)
+    lib.ref_traversal_data(C.byref(os_.s), _p(r), C.c_float(max_dst), C.byref(start), C.byref(scale), _p(idx),
+                           _p(ts))
+    return start.value, scale.value, idx, ts
+
+
 def intersect(scene, rays, last_prim=None, last_normal=None):
     lib = load()
     os_ = OracleScene(scene)
