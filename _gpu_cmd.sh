@@ -1,5 +1,4 @@
 set -e
-echo "== C2"; timeout -k 10 120 python scripts/spp_sweep.py C2 64 --ktime
-echo "== C4"; timeout -k 10 200 python scripts/spp_sweep.py C4 64 --ktime
-echo "== C3 preview"; timeout -k 10 120 python scripts/spp_sweep.py C3 1 1 1 --preview
-echo "== C4 preview"; timeout -k 10 120 python scripts/spp_sweep.py C4 1 1 1 --preview
+timeout -k 10 400 python -m pytest tests -m gpu -x -q 2>&1 | tail -4
+echo "== C5"; OCTPT_DEBUG=1 timeout -k 10 300 python scripts/spp_sweep.py C5 16 64 --ktime
+echo "== C5 preview"; timeout -k 10 120 python scripts/spp_sweep.py C5 1 1 1 --preview

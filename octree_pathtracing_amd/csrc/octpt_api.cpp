@@ -1117,10 +1117,13 @@ octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const 
         // primitive.  Leaf tables index pairs with uint32, and a scene past 2^31 pairs (>= 32 GiB
         // of pairs) is refused up front rather than discovered by allocating until bad_alloc.
         uint64_t bound = 0;
-        auto add_box = [&](const float *lo_f, const float *hi_f) {
+        // cuboid cells span floor(min) .. ceil(max) - 1: a face on an integer plane does not claim
+        // the next cell, so a unit block [x, x+1) is exactly one cell (the voxel world of C5)
+        auto cub_hi = [](float lo, float hi) { return std::max(floorf(lo), ceilf(hi) - 1.0f); };
+        auto add_box = [&](const float *lo_f, const float *hi_f, bool half_open) {
             uint64_t cells = 1;
             for (int a = 0; a < 3; ++a) {
-                const float fl = floorf(lo_f[a]), fh = floorf(hi_f[a]);
+                const float fl = floorf(lo_f[a]), fh = half_open ? cub_hi(lo_f[a], hi_f[a]) : floorf(hi_f[a]);
                 if (fh < 0.0f || fl > (float)(N - 1) || hi_f[a] < lo_f[a]) return;
                 cells *= (uint64_t)(clamp_cell(fh, N - 1) - clamp_cell(fl, N - 1) + 1);
             }
@@ -1130,9 +1133,9 @@ octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const 
             const float *c = spheres[i].center, r = spheres[i].radius;
             if (!(r > 0.0f)) continue;
             const float lo_f[3] = {c[0] - r, c[1] - r, c[2] - r}, hi_f[3] = {c[0] + r, c[1] + r, c[2] + r};
-            add_box(lo_f, hi_f);
+            add_box(lo_f, hi_f, false);
         }
-        for (uint32_t i = 0; i < nc; ++i) add_box(cuboids[i].min, cuboids[i].max);
+        for (uint32_t i = 0; i < nc; ++i) add_box(cuboids[i].min, cuboids[i].max, true);
         if (bound > kMaxBuildPairs) return OCTPT_ERR_OOM;
         std::vector<CellPrim> cells;
         cells.reserve((size_t)std::min<uint64_t>(bound, 1ull << 24));
@@ -1168,7 +1171,7 @@ octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const 
             int32_t lo[3], hi[3];
             bool empty = false;
             for (int a = 0; a < 3; ++a) {
-                const float fl = floorf(b.min[a]), fh = floorf(b.max[a]);
+                const float fl = floorf(b.min[a]), fh = cub_hi(b.min[a], b.max[a]);
                 if (fh < 0.0f || fl > (float)(N - 1) || b.max[a] < b.min[a]) empty = true;
                 lo[a] = clamp_cell(fl, N - 1);
                 hi[a] = clamp_cell(fh, N - 1);

@@ -406,6 +406,81 @@ def textured_materials(scene: Scene, seed: int) -> dict:
     return ids
 
 
+def _value_noise(seed: int, stream: int, h: int, w: int, grids) -> np.ndarray:
+    """Bilinear value noise, octaves with the given (gx, gy) lattice sizes, normalised to [0, 1]."""
+    acc = np.zeros((h, w), np.float32)
+    for o, (gx, gy) in enumerate(grids):
+        g = scene_uniform(seed, stream + o, (gy + 1) * (gx + 1)).reshape(gy + 1, gx + 1)
+        ys = np.linspace(0, gy, h, endpoint=False, dtype=np.float32)
+        xs = np.linspace(0, gx, w, endpoint=False, dtype=np.float32)
+        y0, x0 = ys.astype(np.int64), xs.astype(np.int64)
+        fy, fx = (ys - y0)[:, None], (xs - x0)[None, :]
+        acc += ((g[y0][:, x0] * (1 - fx) + g[y0][:, x0 + 1] * fx) * (1 - fy) +
+                (g[y0 + 1][:, x0] * (1 - fx) + g[y0 + 1][:, x0 + 1] * fx) * fy) / (2 ** o)
+    acc -= acc.min()
+    return acc / acc.max()
+
+
+BLOCK_TILES = {  # base colour, texel noise amplitude, (top rows colour, rows) for side tiles
+    "grass_top": ((95, 159, 53), 30, None), "grass_side": ((134, 96, 67), 24, ((95, 159, 53), 4)),
+    "dirt": ((134, 96, 67), 24, None), "stone": ((125, 125, 125), 30, None),
+    "snow": ((240, 244, 250), 10, None), "snow_side": ((134, 96, 67), 24, ((240, 244, 250), 5)),
+    "sand": ((219, 207, 163), 18, None),
+}
+
+
+def block_tile(seed: int, stream: int, base, amp, top=None) -> np.ndarray:
+    """A 16x16 RGBA8 block texture: base colour + per-texel noise, optionally a differently
+    coloured top band (side faces of grass / snow blocks)."""
+    noise = scene_uniform(seed, stream, 256).reshape(16, 16) * (2 * amp) - amp
+    rgb = np.broadcast_to(np.float32(base), (16, 16, 3)).copy()
+    if top is not None:
+        rgb[: top[1]] = np.float32(top[0])
+    out = np.empty((16, 16, 4), np.uint8)
+    out[..., :3] = np.clip(rgb + noise[..., None], 0, 255).astype(np.uint8)
+    out[..., 3] = 255
+    return out
+
+
+def voxel_terrain(scene: Scene, seed: int, side: int, origin: int = 24):
+    """C5's voxel world: a value-noise heightmap over side x side columns starting
+    at (origin, origin), heights in [48, 176); every column holds its top block plus the blocks a
+    lower neighbour exposes, all unit cubes [x, x+1)^3 (one octree cell each).
+    Faces W, E, Bottom, Top, South, North take materials of 16x16 block textures by block kind:
+    sand below 64, snow from 150, grass otherwise; exposed blocks below the top are dirt (3 deep)
+    then stone.  Returns (cuboids [n, 6], face materials [n, 6])."""
+    if not scene.textures:
+        scene.textures = [Texture()]
+        scene.materials = [air_material(0)]
+    mat = {}
+    for k, (name, (base, amp, top)) in enumerate(BLOCK_TILES.items()):
+        scene.textures.append(Texture.image(block_tile(seed, 300 + k, base, amp, top)))
+        scene.materials.append(Material(texture_index=len(scene.textures) - 1))
+        mat[name] = len(scene.materials) - 1
+    # face order W, E, Bottom, Top, South, North (cuboid.rs:9-29)
+    kinds = np.array([[mat["grass_side"]] * 2 + [mat["dirt"], mat["grass_top"]] + [mat["grass_side"]] * 2,
+                      [mat["dirt"]] * 6, [mat["stone"]] * 6,
+                      [mat["snow_side"]] * 2 + [mat["dirt"], mat["snow"]] + [mat["snow_side"]] * 2,
+                      [mat["sand"]] * 6], np.uint32)
+    hmap = (48 + np.floor(128 * _value_noise(seed, 400, side, side, [(6, 6), (12, 12), (24, 24), (48, 48)])))
+    h = hmap.astype(np.int64)
+    pad = np.pad(h, 1, mode="edge")
+    nbr = np.minimum.reduce([pad[:-2, 1:-1], pad[2:, 1:-1], pad[1:-1, :-2], pad[1:-1, 2:]])
+    lo = np.minimum(h, nbr + 1)  # lowest exposed block of the column
+    count = (h - lo + 1).ravel()
+    zz, xx = np.meshgrid(np.arange(side), np.arange(side), indexing="ij")
+    col = np.repeat(np.arange(side * side), count)
+    first = np.repeat(np.cumsum(count) - count, count)
+    top = h.ravel()[col]
+    y = top - (np.arange(len(col)) - first)
+    below = top - y
+    kind = np.where(below >= 4, 2, np.where(below >= 1, 1, np.where(top >= 150, 3, np.where(top < 64, 4, 0))))
+    x = xx.ravel()[col] + origin
+    z = zz.ravel()[col] + origin
+    lo3 = np.stack([x, y, z], 1).astype(F32)
+    return np.concatenate([lo3, lo3 + F32(1.0)], 1), kinds[kind]
+
+
 def _assign_materials(ids, seed, n, stream=7):
     """70% diffuse, 15% metal, 10% glossy, 5% glass."""
     u = scene_uniform(seed, stream, n)
@@ -431,7 +506,10 @@ def random_cuboids(seed: int, n: int, world: float, emin: float, emax: float):
     return np.concatenate([lo, np.minimum(lo + ext, F32(world - 0.001))], axis=1).astype(F32)
 
 
-CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "tiny")
+CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny")
+
+
+C5_SIDE = 1000  # columns per side: 1,001,225 unit blocks with the exposed-side fill
 
 
 def make_config(name: str, *, seed: int = 1, build: bool = True):
@@ -481,6 +559,12 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
         sc.cuboid_material = _assign_materials(ids, seed + 5, 6 * n, stream=21).reshape(n, 6)
         cam = Camera.look_at((512.0, 600.0, -420.0), (512.0, 512.0, 512.0))
         rs = RenderSettings(3840, 2160, 512, seed=seed)
+    elif name == "C5":
+        depth = 11
+        sc.cuboids, sc.cuboid_material = voxel_terrain(sc, seed, C5_SIDE)
+        mid = 24 + C5_SIDE / 2
+        cam = Camera.look_at((mid, 230.0, 24.0 - 60.0), (mid, 100.0, mid))
+        rs = RenderSettings(3840, 2160, 1024, seed=seed)
     else:
         raise ValueError(f"unknown config {name!r}; known: {CONFIGS}")
     if build:

@@ -1447,7 +1447,9 @@ int ref_build_octree(const float *spheres, uint32_t ns, const float *cuboids, ui
         int32_t lo[3], hi[3];
         int empty = 0;
         for (int a = 0; a < 3; a++) {
-            float fl = floorf(b[a]), fh = floorf(b[3 + a]);
+            /* half-open upper bound: a face on an integer plane does not claim the next cell
+             * (a unit block [x, x+1) is one cell, the voxel world of C5) */
+            float fl = floorf(b[a]), fh = fmaxf(fl, ceilf(b[3 + a]) - 1.0f);
             if (fh < 0.0f || fl > (float)(N - 1) || b[3 + a] < b[a]) empty = 1;
             lo[a] = clampi((int64_t)fmaxf(fl, -1.0f), 0, N - 1);
             hi[a] = clampi((int64_t)fminf(fh, (float)N), 0, N - 1);

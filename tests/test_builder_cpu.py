@@ -21,7 +21,7 @@ def _same(sc):
     return t
 
 
-@pytest.mark.parametrize("name", ["C1", "tiny", "C2", "C3"])
+@pytest.mark.parametrize("name", ["C1", "tiny", "C2", "C3", "C5"])
 def test_builder_configs(name):
     sc, _, _ = S.make_config(name)
     t = _same(sc)
@@ -97,3 +97,16 @@ def test_empty_scene_octree():
     sc.build_octree(4)
     _same(sc)
     assert len(sc.octree.leaf_first) == 0
+
+
+def test_unit_blocks_claim_one_cell():
+    """Cuboid cells are half-open at the top: a unit block [x, x+1)^3 is exactly one
+    leaf cell, a degenerate box on an integer plane still claims its cell, and a box reaching past
+    an integer plane claims both sides."""
+    sc = S.Scene()
+    sc.cuboids = np.array([[3, 3, 3, 4, 4, 4], [5, 5, 5, 5, 5, 5], [0.5, 0.5, 0.5, 2.25, 1.0, 1.0]], np.float32)
+    sc.cuboid_material = np.zeros((3, 6), np.uint32)
+    sc.build_octree(3)
+    t = _same(sc)
+    assert len(t.leaf_first) == 1 + 1 + 3  # x cells 0,1,2 for the third box
+    assert np.all(t.leaf_count == 1)

@@ -11,7 +11,8 @@ from oracle import cpu_ref
 from octree_pathtracing_amd import scene as S
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
-RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c3_preview", "c4_preview"]
+RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c5_small", "c3_preview", "c4_preview",
+           "c5_preview"]
 STAT_KEYS = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
              "texel_reads", "max_path_segs")
 

@@ -89,7 +89,7 @@ def assert_parity(gpu, ref, tag):
 
 
 @pytest.mark.parametrize("name,res", [("tiny", None), ("C1", None), ("C1-as-is", None), ("C2", (160, 90, 8)),
-                                      ("C3", (192, 108, 2)), ("C4", (128, 72, 2))])
+                                      ("C3", (192, 108, 2)), ("C4", (128, 72, 2)), ("C5", (192, 108, 2))])
 def test_render_parity(torch_cuda, renderer, name, res):
     from octree_pathtracing_amd import scene as S
 
@@ -356,8 +356,8 @@ def test_wavefront_small_pool_many_chunks(torch_cuda, renderer):
 GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
 
 
-@pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c3_preview",
-                                  "c4_preview"])
+@pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c5_small",
+                                  "c3_preview", "c4_preview", "c5_preview"])
 def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     """GPU render vs the committed oracle fixture (tests/golden/make_golden.py): exact per-pixel
     segment counts and work totals, radiance within REL_TOL_FORWARD."""
@@ -421,7 +421,7 @@ def test_split_extend_equals_default(torch_cuda, renderer, name, res):
 
 # ---------------------------------------------------------------------------- preview mode (C16)
 @pytest.mark.parametrize("name,res", [("tiny", None), ("C1", None), ("C2", (160, 90)), ("C3", (256, 144)),
-                                      ("C4", (160, 90))])
+                                      ("C4", (160, 90)), ("C5", (320, 180))])
 def test_preview_parity(torch_cuda, renderer, name, res):
     """RendererMode::Preview (preview_kernel) vs the oracle: segment counts, work totals and the
     flat-shaded radiance bit-exact; alpha of the incoming buffer untouched."""
