@@ -155,6 +155,7 @@ typedef struct octpt_stats {
     /* per-kernel HIP-event time of the wavefront loop, renders flagged OCTPT_RENDER_KERNEL_TIMING only */
     uint64_t extend_launches, shade_launches;
     double extend_ms, shade_ms;
+    double build_ms; /* device time (upload excluded) of the last octpt_build_octree_device */
 } octpt_stats;
 
 /* --- library / context ------------------------------------------------------ */
@@ -240,6 +241,14 @@ typedef struct octpt_octree_view {
 } octpt_octree_view;
 octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t sphere_count, const octpt_cuboid *cuboids,
                                 uint32_t cuboid_count, uint32_t depth, octpt_octree **out);
+/* The same builder on the context's device (the reference's flattener
+ * octree_to_gpu_data, gpu_octree.rs:28-76, is todo!()): count / scan / emit (cell, primitive) pairs,
+ * stable radix sort by Morton code, leaf tables, pre-order octant ids by a scan of the octants each
+ * leaf opens.  The result equals octpt_build_octree's array for array.  Inputs are host arrays
+ * (borrowed), the result is a host octree as above. */
+octpt_status octpt_build_octree_device(octpt_ctx *ctx, const octpt_sphere *spheres, uint32_t sphere_count,
+                                       const octpt_cuboid *cuboids, uint32_t cuboid_count, uint32_t depth,
+                                       octpt_octree **out);
 octpt_status octpt_octree_get_view(const octpt_octree *tree, octpt_octree_view *view);
 void octpt_octree_free(octpt_octree *tree);
 

@@ -116,7 +116,7 @@ class Stats(C.Structure):
                 ("sphere_tests", C.c_uint64), ("cuboid_tests", C.c_uint64), ("shade_events", C.c_uint64),
                 ("texel_reads", C.c_uint64), ("launches", C.c_uint64), ("kernel_ms", C.c_double),
                 ("extend_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("extend_ms", C.c_double),
-                ("shade_ms", C.c_double)]
+                ("shade_ms", C.c_double), ("build_ms", C.c_double)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -154,6 +154,7 @@ SIGNATURES = {
     "octpt_get_stats": (_i32, [_vp, C.POINTER(Stats)]),
     "octpt_reset_stats": (_i32, [_vp]),
     "octpt_build_octree": (_i32, [_vp, _u32, _vp, _u32, _u32, C.POINTER(_vp)]),
+    "octpt_build_octree_device": (_i32, [_vp, _vp, _u32, _vp, _u32, _u32, C.POINTER(_vp)]),
     "octpt_octree_get_view": (_i32, [_vp, C.POINTER(OctreeView)]),
     "octpt_octree_free": (None, [_vp]),
 }

@@ -80,6 +80,8 @@ struct octpt_ctx {
     std::vector<EventPair> ev_pool;
     double kern_ms[2] = {0.0, 0.0};
     uint64_t kern_n[2] = {0, 0};
+    float build_ms = 0.0f;  // device time of the last octpt_build_octree_device
+    BuildScratch build_scratch;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
     int extend_bpc_cache[kMaxDepth + 1][2][3] = {};
     // wavefront pool (grown on demand)
@@ -111,11 +113,7 @@ struct octpt_frame {
     bool delivered = false;
 };
 
-struct octpt_octree {
-    std::vector<octpt_octant> octants;
-    std::vector<uint32_t> leaf_first, leaf_count, leaf_prims;
-    uint32_t root = 0, depth = 0;
-};
+struct octpt_octree : octpt::BuiltOctree {};
 
 namespace {
 
@@ -595,6 +593,35 @@ inline int32_t clamp_cell(float f, int32_t hi) {
     return (int32_t)f;
 }
 
+// Upper bound of the (cell, primitive) pairs: the clamped bounding-box cells of every primitive.
+// Leaf tables index pairs with uint32, and a scene past 2^31 pairs (>= 32 GiB of pairs) is refused
+// up front rather than discovered by allocating until bad_alloc.  Cuboid cells span floor(min) ..
+// ceil(max) - 1: a face on an integer plane does not claim the next cell, so a unit block
+// [x, x+1) is exactly one cell (the voxel world of C5).
+uint64_t pair_bound(const octpt_sphere *spheres, uint32_t ns, const octpt_cuboid *cuboids, uint32_t nc,
+                    uint32_t depth) {
+    const int32_t N = 1 << depth;
+    uint64_t bound = 0;
+    auto cub_hi = [](float lo, float hi) { return std::max(floorf(lo), ceilf(hi) - 1.0f); };
+    auto add_box = [&](const float *lo_f, const float *hi_f, bool half_open) {
+        uint64_t cells = 1;
+        for (int a = 0; a < 3; ++a) {
+            const float fl = floorf(lo_f[a]), fh = half_open ? cub_hi(lo_f[a], hi_f[a]) : floorf(hi_f[a]);
+            if (fh < 0.0f || fl > (float)(N - 1) || hi_f[a] < lo_f[a]) return;
+            cells *= (uint64_t)(clamp_cell(fh, N - 1) - clamp_cell(fl, N - 1) + 1);
+        }
+        bound = std::min<uint64_t>(bound + cells, UINT64_MAX / 2);
+    };
+    for (uint32_t i = 0; i < ns; ++i) {
+        const float *c = spheres[i].center, r = spheres[i].radius;
+        if (!(r > 0.0f)) continue;
+        const float lo_f[3] = {c[0] - r, c[1] - r, c[2] - r}, hi_f[3] = {c[0] + r, c[1] + r, c[2] + r};
+        add_box(lo_f, hi_f, false);
+    }
+    for (uint32_t i = 0; i < nc; ++i) add_box(cuboids[i].min, cuboids[i].max, true);
+    return bound;
+}
+
 }  // namespace
 
 extern "C" {
@@ -665,6 +692,7 @@ void octpt_destroy(octpt_ctx *ctx) {
     }
     free_scene(ctx);
     free_wave(ctx);
+    ctx->build_scratch.release();
     if (ctx->h_count) (void)hipHostFree(ctx->h_count);
     for (auto &ev : ctx->count_ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1088,6 +1116,7 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     out->shade_launches = ctx->kern_n[1];
     out->extend_ms = ctx->kern_ms[0];
     out->shade_ms = ctx->kern_ms[1];
+    out->build_ms = ctx->build_ms;
     return OCTPT_OK;
 }
 
@@ -1105,6 +1134,38 @@ octpt_status octpt_reset_stats(octpt_ctx *ctx) {
     return OCTPT_OK;
 }
 
+octpt_status octpt_build_octree_device(octpt_ctx *ctx, const octpt_sphere *spheres, uint32_t ns,
+                                       const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, octpt_octree **out) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    if (!out) return fail(ctx, OCTPT_ERR_INVALID_ARG, "out NULL");
+    *out = nullptr;
+    if (depth < 1 || depth > kMaxDepth) return fail(ctx, OCTPT_ERR_INVALID_ARG, "depth must be in [1, 21]");
+    if ((ns && !spheres) || (nc && !cuboids)) return fail(ctx, OCTPT_ERR_INVALID_ARG, "NULL primitive array");
+    try {
+        join_inflight(ctx);
+        if (pair_bound(spheres, ns, cuboids, nc, depth) > kMaxBuildPairs)
+            return fail(ctx, OCTPT_ERR_OOM, "more than 2^31 (cell, primitive) pairs");
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        octpt_octree *t = new octpt_octree();
+        bool too_many = false;
+        float ms = 0.0f;
+        const hipError_t e = build_octree_gpu(ctx->stream, ctx->build_scratch, spheres, ns, cuboids, nc, depth,
+                                              kMaxBuildPairs, *t, too_many, &ms);
+        if (e != hipSuccess || too_many) {
+            delete t;
+            if (e == hipErrorOutOfMemory || too_many) return fail(ctx, OCTPT_ERR_OOM, "octree build: out of memory");
+            return hip_fail(ctx, e, "octree build");
+        }
+        ctx->build_ms = ms;
+        *out = t;
+        return OCTPT_OK;
+    } catch (const std::bad_alloc &) {
+        return fail(ctx, OCTPT_ERR_OOM, "octree build: host out of memory");
+    } catch (...) {
+        return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in octree build");
+    }
+}
+
 octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const octpt_cuboid *cuboids, uint32_t nc,
                                 uint32_t depth, octpt_octree **out) {
     if (!out) return OCTPT_ERR_INVALID_ARG;
@@ -1113,30 +1174,10 @@ octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const 
     if ((ns && !spheres) || (nc && !cuboids)) return OCTPT_ERR_INVALID_ARG;
     try {
         const int32_t N = 1 << depth;
-        // upper bound of the (cell, primitive) pairs: the clamped bounding-box cells of every
-        // primitive.  Leaf tables index pairs with uint32, and a scene past 2^31 pairs (>= 32 GiB
-        // of pairs) is refused up front rather than discovered by allocating until bad_alloc.
-        uint64_t bound = 0;
-        // cuboid cells span floor(min) .. ceil(max) - 1: a face on an integer plane does not claim
-        // the next cell, so a unit block [x, x+1) is exactly one cell (the voxel world of C5)
-        auto cub_hi = [](float lo, float hi) { return std::max(floorf(lo), ceilf(hi) - 1.0f); };
-        auto add_box = [&](const float *lo_f, const float *hi_f, bool half_open) {
-            uint64_t cells = 1;
-            for (int a = 0; a < 3; ++a) {
-                const float fl = floorf(lo_f[a]), fh = half_open ? cub_hi(lo_f[a], hi_f[a]) : floorf(hi_f[a]);
-                if (fh < 0.0f || fl > (float)(N - 1) || hi_f[a] < lo_f[a]) return;
-                cells *= (uint64_t)(clamp_cell(fh, N - 1) - clamp_cell(fl, N - 1) + 1);
-            }
-            bound = std::min<uint64_t>(bound + cells, UINT64_MAX / 2);
-        };
-        for (uint32_t i = 0; i < ns; ++i) {
-            const float *c = spheres[i].center, r = spheres[i].radius;
-            if (!(r > 0.0f)) continue;
-            const float lo_f[3] = {c[0] - r, c[1] - r, c[2] - r}, hi_f[3] = {c[0] + r, c[1] + r, c[2] + r};
-            add_box(lo_f, hi_f, false);
-        }
-        for (uint32_t i = 0; i < nc; ++i) add_box(cuboids[i].min, cuboids[i].max, true);
+        const uint64_t bound = pair_bound(spheres, ns, cuboids, nc, depth);
         if (bound > kMaxBuildPairs) return OCTPT_ERR_OOM;
+        // cuboid cells are half-open at the top (pair_bound)
+        auto cub_hi = [](float lo, float hi) { return std::max(floorf(lo), ceilf(hi) - 1.0f); };
         std::vector<CellPrim> cells;
         cells.reserve((size_t)std::min<uint64_t>(bound, 1ull << 24));
         for (uint32_t i = 0; i < ns; ++i) {

@@ -4,6 +4,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
+#include <new>
+#include <utility>
+#include <vector>
+
+#include "../../include/octpt.h"
+
 namespace octpt {
 
 constexpr uint32_t kPrimNone = 0xFFFFFFFFu;
@@ -159,5 +166,49 @@ hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const fl
                           uint32_t stride, float4 *frame, hipStream_t stream);
 int render_blocks_per_cu(uint32_t depth);
 size_t render_lds_bytes(uint32_t depth);
+
+// std::vector allocator that leaves resized elements uninitialised: the builders overwrite every
+// element, and zero-filling a C4 octree's 0.2 GB first costs more than the GPU build itself
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new (static_cast<void *>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using RawVec = std::vector<T, NoInitAlloc<T>>;
+
+// host arrays of a built octree (octpt_octree, include/octpt.h)
+struct BuiltOctree {
+    RawVec<octpt_octant> octants;
+    RawVec<uint32_t> leaf_first, leaf_count, leaf_prims;
+    uint32_t root = 0, depth = 0;
+};
+
+// grow-only device scratch of the GPU octree builder, owned by the context: repeated builds
+// (scene edits) reuse it instead of paying hipMalloc / hipFree per buffer
+struct BuildScratch {
+    static constexpr int kSlots = 24;
+    void *dev[kSlots] = {};
+    size_t cap[kSlots] = {};
+    void release();
+};
+
+// the octree builder on the device (octpt_build.hip); too_many: more than max_pairs pairs
+hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const octpt_sphere *spheres, uint32_t ns,
+                            const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, uint64_t max_pairs,
+                            BuiltOctree &out, bool &too_many, float *ms);
 
 }  // namespace octpt

@@ -182,24 +182,31 @@ class Scene:
     octree: Octree | None = None
 
     # ---------------------------------------------------------------- octree
-    def build_octree(self, depth: int) -> Octree:
-        """Voxelise the primitives with the product builder (octpt_build_octree)."""
+    def build_octree(self, depth: int, renderer=None) -> Octree:
+        """Voxelise the primitives with the product builder: octpt_build_octree (host), or with a
+        HipRenderer given, octpt_build_octree_device on its GPU (the same arrays)."""
         lib = _lib.load()
         sph = self.sphere_structs()
         cub = self.cuboid_structs()
         handle = C.c_void_p()
-        st = lib.octpt_build_octree(C.cast(sph, C.c_void_p) if len(self.spheres) else None, len(self.spheres),
-                                    C.cast(cub, C.c_void_p) if len(self.cuboids) else None, len(self.cuboids),
-                                    depth, C.byref(handle))
-        _lib.check(lib, None, st)
+        args = (C.cast(sph, C.c_void_p) if len(self.spheres) else None, len(self.spheres),
+                C.cast(cub, C.c_void_p) if len(self.cuboids) else None, len(self.cuboids), depth, C.byref(handle))
+        if renderer is None:
+            _lib.check(lib, None, lib.octpt_build_octree(*args))
+        else:
+            _lib.check(lib, renderer._ctx, lib.octpt_build_octree_device(renderer._ctx, *args))
         try:
             v = _lib.OctreeView()
             _lib.check(lib, None, lib.octpt_octree_get_view(handle, C.byref(v)))
             dt = np.dtype([("m", "<u2"), ("r", "<u2"), ("c", "<u4", (8,))])
-            oct_ = np.frombuffer(C.string_at(v.octants, 36 * v.octant_count), dtype=dt)
+
+            def view(ptr, nbytes):  # zero-copy view of library memory (copied out below)
+                return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
+
+            oct_ = view(v.octants, 36 * v.octant_count).view(dt)
 
             def u32(ptr, n):
-                return np.frombuffer(C.string_at(ptr, 4 * n), dtype=np.uint32).copy() if n else np.zeros(0, np.uint32)
+                return view(ptr, 4 * n).view(np.uint32).copy() if n else np.zeros(0, np.uint32)
 
             self.octree = Octree(oct_["m"].copy(), oct_["c"].copy(), int(v.root), int(v.depth),
                                  u32(v.leaf_first, v.leaf_table_size), u32(v.leaf_count, v.leaf_table_size),

@@ -1,0 +1,66 @@
+"""GPU octree builder (octpt_build_octree_device, csrc/octpt_build.hip) against the host builder
+(octpt_build_octree, itself pinned to the oracle builder by tests/test_builder_cpu.py): identical
+octants, child words, leaf tables and primitive lists, bit for bit."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def renderer():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    r = HipRenderer(device=0)
+    yield r
+    r.close()
+
+
+def _same(sc, depth, renderer):
+    host = sc.build_octree(depth)
+    dev = sc.build_octree(depth, renderer=renderer)
+    assert dev.root == host.root and dev.depth == host.depth
+    for k in ("octant_mask", "octant_children", "leaf_first", "leaf_count", "leaf_prims"):
+        assert np.array_equal(getattr(dev, k), getattr(host, k)), k
+    return dev
+
+
+@pytest.mark.parametrize("name", ["C1", "tiny", "C2", "C3", "C4", "C5"])
+def test_device_builder_configs(renderer, name):
+    from octree_pathtracing_amd import scene as S
+
+    sc, _, _ = S.make_config(name, build=False)
+    t = _same(sc, sc._depth, renderer)
+    assert t.octant_count > 0 and len(t.leaf_first) > 0
+
+
+@pytest.mark.parametrize("seed,depth", [(1, 1), (2, 3), (3, 9), (4, 12), (5, 21)])
+def test_device_builder_random(renderer, seed, depth):
+    from octree_pathtracing_amd import scene as S
+
+    world = float(1 << depth)
+    sc = S.Scene()
+    sc.spheres = S.random_spheres(seed, 300, world * 1.1, 0.01, min(max(world / 6, 0.6), 6.0))
+    sc.sphere_material = np.zeros(300, np.uint32)
+    sc.cuboids = S.random_cuboids(seed, 50, world, 0.2, min(max(world / 5, 0.5), 8.0))
+    sc.cuboids[:5] = np.floor(sc.cuboids[:5])  # integer faces: the half-open bound
+    sc.cuboid_material = np.zeros((50, 6), np.uint32)
+    _same(sc, depth, renderer)
+
+
+def test_device_builder_empty_and_oom(renderer):
+    from octree_pathtracing_amd import _lib
+    from octree_pathtracing_amd import scene as S
+
+    sc = S.Scene()
+    t = _same(sc, 4, renderer)
+    assert t.octant_count == 1 and len(t.leaf_first) == 0
+    big = S.Scene()
+    big.cuboids = np.array([[0, 0, 0, 2047.5, 2047.5, 2047.5]], np.float32)  # 2^33 cells
+    big.cuboid_material = np.zeros((1, 6), np.uint32)
+    with pytest.raises(_lib.OctptError) as e:
+        big.build_octree(11, renderer=renderer)
+    assert e.value.status == _lib.ERR_OOM
