@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTPT_ABI_VERSION 1u
+#define OCTPT_ABI_VERSION 2u
 
 typedef int32_t octpt_status;
 #define OCTPT_OK 0
@@ -93,7 +93,11 @@ typedef struct octpt_sun {
     float importance_sample_chance, importance_sample_radius;
     float luminosity;
     uint8_t texture_rgba[4];
-    int32_t importance_sampling, diffuse_sun, sun_sampling; /* sun_sampling=1 -> UNSUPPORTED */
+    int32_t importance_sampling, diffuse_sun;
+    /* next-event estimation toward the sun (do_diffuse_reflection, path_tracer.rs:225-291;
+     * get_direct_light_attenuation :458-483): presets FAST / HIGH_QUALITY (scene/mod.rs:98-126) */
+    int32_t sun_sampling, strict_direct_light, sun_luminosity;
+    float luminosity_pdf; /* Sun::luminosity_pdf, 1/100 in Sun::new (scene/mod.rs:376) */
 } octpt_sun;
 
 /* Scene (src/scene/mod.rs:146-156) flattened: octree + leaf primitive lists + primitive,
@@ -118,6 +122,7 @@ typedef struct octpt_scene_desc {
     uint32_t texture_count;
     octpt_sun sun;
     int32_t emitters_enabled;
+    float f_sub_surface; /* Scene::f_sub_surface (scene/mod.rs:152): subsurface sun-sample chance */
 } octpt_scene_desc;
 
 /* renderer::camera::Camera (src/renderer/camera.rs:8-25) */

@@ -13,7 +13,7 @@ from pathlib import Path
 LIB_DIR = Path(__file__).resolve().parent / "lib"
 LIB_PATH = LIB_DIR / "liboctpt.so"
 
-OCTPT_ABI_VERSION = 1
+OCTPT_ABI_VERSION = 2
 
 OK = 0
 ERR_INVALID_ARG = 1
@@ -85,7 +85,8 @@ class Sun(C.Structure):
         ("apparent_color", C.c_float * 3), ("draw_texture", C.c_int32), ("texture_modification", C.c_int32),
         ("importance_sample_chance", C.c_float), ("importance_sample_radius", C.c_float), ("luminosity", C.c_float),
         ("texture_rgba", C.c_uint8 * 4), ("importance_sampling", C.c_int32), ("diffuse_sun", C.c_int32),
-        ("sun_sampling", C.c_int32),
+        ("sun_sampling", C.c_int32), ("strict_direct_light", C.c_int32), ("sun_luminosity", C.c_int32),
+        ("luminosity_pdf", C.c_float),
     ]
 
 
@@ -96,7 +97,7 @@ class SceneDesc(C.Structure):
         ("leaf_table_size", C.c_uint32), ("leaf_prims", C.c_void_p), ("leaf_prim_count", C.c_uint32),
         ("spheres", C.c_void_p), ("sphere_count", C.c_uint32), ("cuboids", C.c_void_p), ("cuboid_count", C.c_uint32),
         ("materials", C.c_void_p), ("material_count", C.c_uint32), ("textures", C.c_void_p),
-        ("texture_count", C.c_uint32), ("sun", Sun), ("emitters_enabled", C.c_int32),
+        ("texture_count", C.c_uint32), ("sun", Sun), ("emitters_enabled", C.c_int32), ("f_sub_surface", C.c_float),
     ]
 
 

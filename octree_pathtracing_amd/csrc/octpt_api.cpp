@@ -191,6 +191,10 @@ void make_sun(const octpt_sun &p, const float lut_float[256], DevSun &k) {
     k.draw_texture = p.draw_texture ? 1 : 0;
     k.importance_sampling = p.importance_sampling ? 1 : 0;
     k.diffuse_sun = p.diffuse_sun ? 1 : 0;
+    k.sun_sampling = p.sun_sampling ? 1 : 0;
+    k.strict_direct_light = p.strict_direct_light ? 1 : 0;
+    k.lum_a = p.sun_luminosity ? p.luminosity_pdf : 1.0f;  // path_tracer.rs:250-254
+    k.radius_cos = cosf(p.radius);                          // Sun::new (scene/mod.rs:331)
 }
 
 void free_scene(octpt_ctx *ctx) {
@@ -252,8 +256,6 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d) {
         return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^27 - 1 spheres or cuboids");
     if (d->sphere_count && !d->spheres) return fail(ctx, OCTPT_ERR_INVALID_ARG, "spheres is NULL");
     if (d->cuboid_count && !d->cuboids) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboids is NULL");
-    if (d->sun.sun_sampling)
-        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "sun_sampling (next-event estimation presets FAST/HIGH_QUALITY) is not implemented");
     for (uint32_t n = 0; n < d->octant_count; ++n) {
         const octpt_octant &o = d->octants[n];
         for (int i = 0; i < 8; ++i) {
@@ -386,6 +388,8 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pa));
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pb));
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pc));
+        HIP_TRY(ctx, wave_alloc(ctx, 4 * pool, &B.pd));
+        B.pool = (uint32_t)pool;
         HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.hit));
         HIP_TRY(ctx, wave_alloc(ctx, kCtrlWords, &B.ctrl));
         ctx->pool = pool;
@@ -835,6 +839,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.texels = d_texels;
         S.lut_float = ctx->d_lut_float;
         make_sun(d->sun, lf, S.sun);
+        S.sun.f_sub_surface = d->f_sub_surface;
         S.emitters = d->emitters_enabled ? 1 : 0;
         ctx->S = S;
         ctx->has_scene = true;

@@ -52,6 +52,11 @@ struct DevSun {
     float sun_dx, sun_dy, sun_dz;
     float circle_radius, sample_chance;
     int32_t draw_texture, importance_sampling, diffuse_sun;
+    // next-event estimation (path_tracer.rs:225-291, 458-483)
+    int32_t sun_sampling, strict_direct_light;
+    float lum_a;          // sun_luminosity ? luminosity_pdf : 1
+    float radius_cos;     // Sun::radius_cos
+    float f_sub_surface;  // Scene::f_sub_surface
 };
 
 struct DevScene {
@@ -119,6 +124,10 @@ struct WaveBuffers {
     uint2 *pc;      // (cur_mat, depth | specular << 8 | path_segs << 16)
     uint2 *hit;     // per queue position: (cuboid bit | flags << 27 | prim index, t) -- hit_record()
     float4 *color;  // per chunk item: (L.xyz, path segments)
+    // sun-sampling state, 4 planes of `pool` float4:
+    // (co.xyz, clast), (cd.xyz, ccur), (cn.xyz, mult), att
+    float4 *pd;
+    uint32_t pool;
     uint32_t *ctrl;    // kCtrlWords sharded counters (see above)
     uint32_t seg_cap;  // positions per queue segment (multiple of 64)
 };

@@ -30,6 +30,7 @@ namespace {
 #define CELL_TOL 0.001f
 #define SUN_MAX_CHANCE 0.9f
 #define MAT_FLAG_REFRACTIVE 0x4u
+#define MAT_FLAG_SUBSURFACE 0x2u  // MaterialFlags::SUBSURFACE_SCATTER (material.rs:9)
 #define MAX_PATH_SEGMENTS 64u  // [C15] next_intersection calls per path (grazing self-hit loops)
 
 // ---------------------------------------------------------------------------
@@ -196,6 +197,14 @@ struct PathState {
     v3 T, L;
     uint32_t cur, prev, depth, last_prim, path_segs, rng;
     bool specular;
+    // next-event estimation (sun sampling), used by the kNee instances only: while
+    // `shadow` is set the ray is a get_direct_light_attenuation segment carrying `att`; the diffuse
+    // bounce it interrupts waits in (co, cd, cn, clast, ccur), `mult` = |d_sun . n| * lum_a
+    bool shadow;
+    float att[4];
+    float mult;
+    v3 co, cd, cn;
+    uint32_t clast, ccur;
 };
 
 struct Esvo {
@@ -651,7 +660,10 @@ __device__ inline void specular_reflection(PathState &r, float roughness) {
     }
 }
 
-__device__ inline void diffuse_reflection(const DevSun &K, PathState &r) {
+// returns the factor the importance-sampling branches multiply ray.hit.color by (ray/mod.rs:262,
+// 276, 297, 307), 1 when none applies; only the sun-sampling caller uses it [C5]
+__device__ inline float diffuse_reflection(const DevSun &K, PathState &r) {
+    float w = 1.0f;
     const v3 n = r.n;
     const v3 d_in = r.d;
     r.col[0] = r.col[1] = r.col[2] = r.col[3] = 0.0f;  // new_from_self
@@ -683,6 +695,7 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathState &r) {
                 if (rng_next(r.rng) < chance) {
                     tx = stx + tx * cr;
                     ty = sty + ty * cr;
+                    w = cr * cr / chance;
                 } else {
                     while (dm_hypot(tx - stx, ty - sty) < cr) {
                         tx -= stx;
@@ -691,6 +704,7 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathState &r) {
                         tx /= cr;
                         ty /= cr;
                     }
+                    w = (1.0f - cr * cr) / (1.0f - chance);
                 }
             } else {
                 const float min_r = dm_cos(alt_rel + cr);
@@ -702,6 +716,7 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathState &r) {
                 if (rng_next(r.rng) < chance) {
                     rr = sqrtf(min_r * min_r * x1 + max_r * max_r * (1.0f - x1));
                     theta = sun_theta + (2.0f * x2 - 1.0f) * cr;
+                    w = seg / chance;
                 } else {
                     for (;;) {
                         if (!(rr > min_r && rr < max_r)) break;
@@ -714,6 +729,7 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathState &r) {
                         rr = sqrtf(x1);
                         theta = 2.0f * PI_F * x2;
                     }
+                    w = (1.0f - seg) / (1.0f - chance);
                 }
                 dm_sincos(theta, sn, cs);
                 tx = rr * cs;
@@ -736,6 +752,21 @@ __device__ inline void diffuse_reflection(const DevSun &K, PathState &r) {
         const float factor = signum_(vdot(n, d_in)) * -RAY_EPSILON - vdot(r.d, n);
         r.d = vnorm(vadd(r.d, vscale(n, factor)));
     }
+    return w;
+}
+
+// Sun::get_random_sun_direction (scene/mod.rs:427-445): (u + v) + normalize(w), not normalised
+__device__ inline v3 random_sun_direction(const DevSun &K, uint32_t &rng) {
+    const float x1 = rng_next(rng), x2 = rng_next(rng);
+    const float cos_a = (1.0f - x1) + x1 * K.radius_cos;
+    const float sin_a = sqrtf(1.0f - cos_a * cos_a);
+    const float phi = 2.0f * PI_F * x2;
+    float sn, cs;
+    dm_sincos(phi, sn, cs);
+    const v3 u = vscale(V(K.su[0], K.su[1], K.su[2]), cs * sin_a);
+    const v3 v = vscale(V(K.sv[0], K.sv[1], K.sv[2]), sn * sin_a);
+    const v3 w = vscale(V(K.sw[0], K.sw[1], K.sw[2]), cos_a);
+    return vadd(vadd(u, v), vnorm(w));
 }
 
 // ---------------------------------------------------------------------------
@@ -763,6 +794,7 @@ __device__ inline void new_path(const DevCamera &C, const DevRender &R, uint32_t
     ps.last_prim = kPrimNone;
     ps.path_segs = 0u;
     ps.specular = true;
+    ps.shadow = false;
 }
 
 // next_intersection prologue (path_tracer.rs:438-446) + Scene::hit direction guard
@@ -781,10 +813,46 @@ __device__ __forceinline__ TraceRay trace_ray_of(const DevScene &S, const PathSt
     return make_trace_ray(S, ps.o, ps.d, ps.last_prim, vdot(ps.d, ps.n) < 0.0f);
 }
 
+// get_direct_light_attenuation (path_tracer.rs:458-483) after one shadow segment: attenuate by the
+// hit's colour and alpha; while light passes, the next shadow segment starts `OFFSET` past the hit.
+// Once it is blocked or escapes, add the sun's direct light and resume the waiting diffuse bounce.
+__device__ inline void shadow_segment_done(const DevScene &S, PathState &ray, bool hit) {
+    if (hit) {
+        const float m = 1.0f - ray.col[3];
+        for (int i = 0; i < 3; ++i) ray.att[i] *= ray.col[i] * ray.col[3] + m;
+        ray.att[3] *= m;
+        if (S.sun.strict_direct_light && S.mats[ray.prev].ior != S.mats[ray.cur].ior) ray.att[3] = 0.0f;
+        if (ray.att[3] > 0.0f) {
+            ray.o = vadd(ray.o, vscale(ray.d, RAY_OFFSET));
+            return;
+        }
+    }
+    if (ray.att[3] > 0.0f) {
+        const float *e = S.sun.emit;
+        v3 &L = ray.L;
+        const v3 T = ray.T;
+        L = V(L.x + T.x * (((ray.att[0] * ray.att[3]) * ray.mult) * e[0]),
+              L.y + T.y * (((ray.att[1] * ray.att[3]) * ray.mult) * e[1]),
+              L.z + T.z * (((ray.att[2] * ray.att[3]) * ray.mult) * e[2]));
+    }
+    ray.shadow = false;
+    ray.o = ray.co;
+    ray.d = ray.cd;
+    ray.n = ray.cn;
+    ray.last_prim = ray.clast;
+    ray.cur = ray.ccur;
+}
+
 // path_tracer.rs:15-135 in forward-throughput form, from a finished segment to either the
-// next segment's ray (returns true) or the end of the path (returns false).
+// next segment's ray (returns true) or the end of the path (returns false).  kNee: the scene may
+// sample the sun; shadow segments run between a diffuse hit and its bounce.
+template <bool kNee>
 __device__ inline bool shade_segment(const DevScene &S, const DevRender &R, PathState &ray, bool hit,
                                      Counters &cnt) {
+    if (kNee && ray.shadow) {
+        shadow_segment_done(S, ray, hit);
+        return true;
+    }
     if (!hit) {
         float sky[3];
         sky_color(S.sun, ray, sky);
@@ -813,6 +881,36 @@ __device__ inline bool shade_segment(const DevScene &S, const DevRender &R, Path
             const v3 e = V(ray.col[0] * ray.col[0] * m.emittance, ray.col[1] * ray.col[1] * m.emittance,
                            ray.col[2] * ray.col[2] * m.emittance);
             ray.L = V(ray.L.x + T.x * e.x, ray.L.y + T.y * e.y, ray.L.z + T.z * e.z);
+        }
+        if (kNee && S.sun.sun_sampling) {
+            // do_diffuse_reflection's sun-sampling branch (path_tracer.rs:225-291).  Draw order:
+            // sun direction, subsurface chance, then the bounce; the shadow loop draws nothing,
+            // so the bounce is drawn now and waits while its shadow segments run
+            const v3 n = ray.n;
+            const v3 sd = random_sun_direction(S.sun, ray.rng);
+            const bool front = vdot(sd, n) > 0.0f;
+            const bool cast = front || ((m.flags & MAT_FLAG_SUBSURFACE) && rng_next(ray.rng) < S.sun.f_sub_surface);
+            const v3 so = front ? ray.o : vadd(ray.o, vscale(n, -RAY_OFFSET));
+            const uint32_t scur = ray.prev;
+            const float mult = fabsf(vdot(sd, n)) * S.sun.lum_a;
+            const float c0 = ray.col[0], c1 = ray.col[1], c2 = ray.col[2];
+            const float w = diffuse_reflection(S.sun, ray);
+            T = V(T.x * (c0 * w), T.y * (c1 * w), T.z * (c2 * w));
+            if (cast) {
+                ray.co = ray.o;
+                ray.cd = ray.d;
+                ray.cn = n;
+                ray.clast = ray.last_prim;
+                ray.ccur = ray.cur;
+                ray.mult = mult;
+                ray.att[0] = ray.att[1] = ray.att[2] = ray.att[3] = 1.0f;
+                ray.shadow = true;
+                ray.o = vadd(so, vscale(sd, RAY_OFFSET));
+                ray.d = sd;
+                ray.n = n;
+                ray.cur = scur;
+            }
+            return true;
         }
         T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
         diffuse_reflection(S.sun, ray);
@@ -913,6 +1011,7 @@ __device__ __forceinline__ uint32_t wave_ticket(uint32_t *ctr, bool want) {
 // ===========================================================================
 enum : uint32_t { ST_IDLE = 0, ST_NEWPATH, ST_BEGIN, ST_TRAV, ST_HIT, ST_MISS, ST_FINISH, ST_DONE };
 
+template <bool kNee>
 __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C, DevRender R, float4 *__restrict__ accum,
                                                         uint32_t *__restrict__ segcount, uint32_t *__restrict__ counter,
                                                         unsigned long long *__restrict__ stats) {
@@ -988,7 +1087,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             bool cont = false;
             if (state != ST_FINISH) {
                 if (state == ST_HIT) commit_hit(S, ray, hprim, hh, cnt);
-                cont = shade_segment(S, R, ray, state == ST_HIT, cnt);
+                cont = shade_segment<kNee>(S, R, ray, state == ST_HIT, cnt);
             }
             if (cont) {
                 state = ST_BEGIN;
@@ -1102,7 +1201,28 @@ __device__ __forceinline__ void store_ray(const WaveBuffers &B, uint32_t q, uint
 __device__ __forceinline__ void store_path(const WaveBuffers &B, uint32_t slot, const PathState &ps, uint32_t item) {
     B.pa[slot] = make_float4(ps.T.x, ps.T.y, ps.T.z, ps.L.x);
     B.pb[slot] = make_float4(ps.L.y, ps.L.z, __uint_as_float(ps.rng), __uint_as_float(item));
-    B.pc[slot] = make_uint2(ps.cur, ps.depth | (ps.specular ? 1u << 8 : 0u) | (ps.path_segs << 16));
+    B.pc[slot] = make_uint2(ps.cur, ps.depth | (ps.specular ? 1u << 8 : 0u) | (ps.shadow ? 1u << 9 : 0u) |
+                                        (ps.path_segs << 16));
+}
+
+// sun-sampling state of a slot (kNee): the waiting bounce + mult, and the attenuation
+__device__ __forceinline__ void store_nee(const WaveBuffers &B, uint32_t slot, const PathState &ps) {
+    B.pd[slot] = make_float4(ps.co.x, ps.co.y, ps.co.z, __uint_as_float(ps.clast));
+    B.pd[B.pool + slot] = make_float4(ps.cd.x, ps.cd.y, ps.cd.z, __uint_as_float(ps.ccur));
+    B.pd[2u * B.pool + slot] = make_float4(ps.cn.x, ps.cn.y, ps.cn.z, ps.mult);
+}
+__device__ __forceinline__ void store_att(const WaveBuffers &B, uint32_t slot, const PathState &ps) {
+    B.pd[3u * B.pool + slot] = make_float4(ps.att[0], ps.att[1], ps.att[2], ps.att[3]);
+}
+__device__ __forceinline__ void load_nee(const WaveBuffers &B, uint32_t slot, PathState &ps) {
+    const float4 a = B.pd[slot], b = B.pd[B.pool + slot], c = B.pd[2u * B.pool + slot], d = B.pd[3u * B.pool + slot];
+    ps.co = V(a.x, a.y, a.z);
+    ps.clast = __float_as_uint(a.w);
+    ps.cd = V(b.x, b.y, b.z);
+    ps.ccur = __float_as_uint(b.w);
+    ps.cn = V(c.x, c.y, c.z);
+    ps.mult = c.w;
+    ps.att[0] = d.x; ps.att[1] = d.y; ps.att[2] = d.z; ps.att[3] = d.w;
 }
 
 __device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, float4 r0, float4 r1, PathState &ps,
@@ -1120,6 +1240,7 @@ __device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, f
     ps.prev = c.x;  // begin_segment set prev = cur before this segment was traced
     ps.depth = c.y & 255u;
     ps.specular = (c.y >> 8) & 1u;
+    ps.shadow = (c.y >> 9) & 1u;
     ps.path_segs = c.y >> 16;
 }
 
@@ -1461,6 +1582,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
 #ifndef OCTPT_SHADE_WAVES
 #define OCTPT_SHADE_WAVES 1
 #endif
+template <bool kNee>
 __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene S, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items,
                                                           unsigned long long *__restrict__ stats) {
@@ -1484,6 +1606,8 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
             const float4 r0 = B.ray0[q][i], r1 = B.ray1[q][i];
             slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
             load_path(B, slot, r0, r1, ps, item);
+            const bool was_shadow = kNee && ps.shadow;
+            if (was_shadow) load_nee(B, slot, ps);
             const uint2 hr = B.hit[i];
             const bool hit = hr.x != kPrimNone;
             if (hit) {
@@ -1494,10 +1618,14 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
                 ps.n = V(0.0f, 0.0f, 0.0f);
                 commit_hit(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
             }
-            bool cont = shade_segment(S, R, ps, hit, cnt);
+            bool cont = shade_segment<kNee>(S, R, ps, hit, cnt);
             if (cont) cont = begin_segment(ps);
             if (cont) {
                 store_path(B, slot, ps, item);
+                if (kNee && ps.shadow) {  // a shadow segment follows: new sun sample or the next one
+                    if (!was_shadow) store_nee(B, slot, ps);
+                    store_att(B, slot, ps);
+                }
                 append = true;
             } else {
                 B.color[item] = make_float4(ps.L.x, ps.L.y, ps.L.z, __uint_as_float(ps.path_segs));
@@ -1606,8 +1734,8 @@ size_t render_lds_bytes(uint32_t depth) { return (size_t)(depth - 1u) * kBlock *
 
 int render_blocks_per_cu(uint32_t depth) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void *>(render_kernel), kBlock,
-                                                     render_lds_bytes(depth)) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void *>(render_kernel<true>),
+                                                     kBlock, render_lds_bytes(depth)) != hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
 }
@@ -1648,8 +1776,12 @@ hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender
 
 hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum, uint32_t *segcount,
                          uint32_t *counter, unsigned long long *stats, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R, accum,
-                       segcount, counter, stats);
+    if (S.sun.sun_sampling)
+        hipLaunchKernelGGL(render_kernel<true>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R,
+                           accum, segcount, counter, stats);
+    else
+        hipLaunchKernelGGL(render_kernel<false>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R,
+                           accum, segcount, counter, stats);
     return hipGetLastError();
 }
 
@@ -1672,7 +1804,10 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
 
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
                            uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream) {
-    hipLaunchKernelGGL(wf_shade_kernel, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
+    if (S.sun.sun_sampling)
+        hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
+    else
+        hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
     return hipGetLastError();
 }
 

@@ -74,6 +74,28 @@ STRATEGY_NON_LUMINOUS = SunSamplingStrategy(False, False, False, False, False)
 STRATEGY_FAST = SunSamplingStrategy(True, False, False, False, False)
 STRATEGY_IMPORTANCE = SunSamplingStrategy(False, True, False, True, True)
 STRATEGY_HIGH_QUALITY = SunSamplingStrategy(True, True, True, True, False)
+STRATEGIES = {"OFF": STRATEGY_OFF, "NON_LUMINOUS": STRATEGY_NON_LUMINOUS, "FAST": STRATEGY_FAST,
+              "IMPORTANCE": STRATEGY_IMPORTANCE, "HIGH_QUALITY": STRATEGY_HIGH_QUALITY}
+
+# sun-sampling test variants: name -> (strategy, set SUBSURFACE_SCATTER on opaque materials)
+SUN_VARIANTS = {
+    "fast": (STRATEGY_FAST, False),
+    "hq": (STRATEGY_HIGH_QUALITY, False),
+    "hq_sss": (STRATEGY_HIGH_QUALITY, True),
+    # sun sampling with importance-sampled bounces: the one combination whose weights are kept
+    "nee_importance": (SunSamplingStrategy(True, True, False, True, True), False),
+}
+
+
+def with_sun_variant(scene: "Scene", variant: str) -> "Scene":
+    """Switch a scene to one of SUN_VARIANTS in place (the octree is unaffected) and return it."""
+    strategy, sss = SUN_VARIANTS[variant]
+    scene.strategy = SunSamplingStrategy(**vars(strategy))
+    if sss:
+        for m in scene.materials:
+            if m.flags & OPAQUE:
+                m.flags |= SUBSURFACE_SCATTER
+    return scene
 
 
 @dataclass
@@ -90,6 +112,7 @@ class Sun:
     importance_sample_chance: float = 0.1
     importance_sample_radius: float = 1.2
     luminosity: float = 100.0
+    luminosity_pdf: float = 1.0 / 100.0  # Sun::new hard-codes 1/100 (scene/mod.rs:376)
 
 
 @dataclass
@@ -179,6 +202,7 @@ class Scene:
     sun: Sun = field(default_factory=Sun)
     strategy: SunSamplingStrategy = field(default_factory=lambda: STRATEGY_IMPORTANCE)
     emitters_enabled: bool = True
+    f_sub_surface: float = 0.3  # Scene::f_sub_surface (scene/mod.rs:152), used by sun sampling (path_tracer.rs:240)
     octree: Octree | None = None
 
     # ---------------------------------------------------------------- octree
@@ -242,7 +266,8 @@ class Scene:
         return _lib.Sun(s.azimuth, s.altitude, s.radius, (C.c_float * 4)(*s.color), (C.c_float * 3)(*s.apparent_color),
                         int(s.draw_texture), int(s.texture_modification), s.importance_sample_chance,
                         s.importance_sample_radius, s.luminosity, (C.c_uint8 * 4)(*s.texture_rgba),
-                        int(st.importance_sampling), int(st.diffuse_sun), int(st.sun_sampling))
+                        int(st.importance_sampling), int(st.diffuse_sun), int(st.sun_sampling),
+                        int(st.strict_direct_light), int(st.sun_luminosity), s.luminosity_pdf)
 
     def to_desc(self):
         """octpt_scene_desc for octpt_scene_upload; returns (desc, keepalive)."""
@@ -296,6 +321,7 @@ class Scene:
         desc.texture_count = len(self.textures)
         desc.sun = self.sun_struct()
         desc.emitters_enabled = int(self.emitters_enabled)
+        desc.f_sub_surface = self.f_sub_surface
         keep.extend([octs, mats, texs])
         return desc, keep
 

@@ -34,6 +34,7 @@
 #define PRIM_NONE 0xFFFFFFFFu
 #define PRIM_CUBOID_BIT 0x80000000u
 #define MAT_FLAG_REFRACTIVE 0x4u     /* src/textures/material.rs:104 */
+#define MAT_FLAG_SUBSURFACE 0x2u     /* MaterialFlags::SUBSURFACE_SCATTER, src/textures/material.rs:9 */
 #ifndef MAX_PATH_SEGMENTS
 #define MAX_PATH_SEGMENTS 64u        /* [C15] next_intersection calls per path */
 #endif
@@ -273,6 +274,10 @@ typedef struct {
     /* diffuse_reflection importance sampling (ray/mod.rs:227-258) */
     float sun_dx, sun_dy, sun_dz, circle_radius, sample_chance;
     int importance_sampling, diffuse_sun;
+    /* next-event estimation (path_tracer.rs:225-291, 458-483) */
+    int sun_sampling, strict_direct_light;
+    float lum_a;      /* sun_luminosity ? luminosity_pdf : 1 (path_tracer.rs:250-254) */
+    float radius_cos; /* Sun::radius_cos (scene/mod.rs:331) */
 } sun_k;
 
 typedef struct {
@@ -325,6 +330,10 @@ static void sun_init(const ref_sun *p, sun_k *k) {
     k->sample_chance = p->importance_sample_chance;
     k->importance_sampling = p->importance_sampling;
     k->diffuse_sun = p->diffuse_sun;
+    k->sun_sampling = p->sun_sampling;
+    k->strict_direct_light = p->strict_direct_light;
+    k->lum_a = p->sun_luminosity ? p->luminosity_pdf : 1.0f;
+    k->radius_cos = cosf(p->radius);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -753,9 +762,12 @@ static void specular_reflection(const ray_t *self, float roughness, uint32_t *rn
     }
 }
 
-/* Ray::diffuse_reflection, :211-373 (self = next, ray = parent). Weight updates of
- * ray.hit.color are discarded by the caller [C5], so they are not modelled. */
-static void diffuse_reflection(ctx_t *c, ray_t *self, const ray_t *ray, uint32_t *rng) {
+/* Ray::diffuse_reflection, :211-373 (self = next, ray = parent).  Returns the factor the
+ * importance-sampling branches multiply ray.hit.color by (:262, 276, 297, 307; 1 when none
+ * applies).  do_diffuse_reflection discards it when the sun is not sampled [C5] and uses it when
+ * it is (:292 reads ray.hit.color after the call). */
+static float diffuse_reflection(ctx_t *c, ray_t *self, const ray_t *ray, uint32_t *rng) {
+    float w = 1.0f;
     const sun_k *k = &c->sun;
     new_from_self(ray, self);
     v3 n = self->n;
@@ -784,6 +796,7 @@ static void diffuse_reflection(ctx_t *c, ray_t *self, const ray_t *ray, uint32_t
                 if (ref_rng_next(rng) < chance) {
                     tx = stx + tx * cr;
                     ty = sty + ty * cr;
+                    w = cr * cr / chance;
                 } else {
                     while (ref_math_hypot(tx - stx, ty - sty) < cr) {
                         tx -= stx;
@@ -792,6 +805,7 @@ static void diffuse_reflection(ctx_t *c, ray_t *self, const ray_t *ray, uint32_t
                         tx /= cr;
                         ty /= cr;
                     }
+                    w = (1.0f - cr * cr) / (1.0f - chance);
                 }
             } else {
                 float min_r = ref_math_cos(alt_rel + cr);
@@ -805,6 +819,7 @@ static void diffuse_reflection(ctx_t *c, ray_t *self, const ray_t *ray, uint32_t
                     theta = sun_theta + (2.0f * x2 - 1.0f) * cr;
                     tx = r * ref_math_cos(theta);
                     ty = r * ref_math_sin(theta);
+                    w = seg / chance;
                 } else {
                     for (;;) {
                         if (!(r > min_r && r < max_r)) break;
@@ -820,6 +835,7 @@ static void diffuse_reflection(ctx_t *c, ray_t *self, const ray_t *ray, uint32_t
                     }
                     tx = r * ref_math_cos(theta);
                     ty = r * ref_math_sin(theta);
+                    w = (1.0f - seg) / (1.0f - chance);
                 }
             }
         }
@@ -840,6 +856,7 @@ static void diffuse_reflection(ctx_t *c, ray_t *self, const ray_t *ray, uint32_t
         float factor = signum_(vdot(n, ray->d)) * -RAY_EPSILON - vdot(self->d, self->n);
         self->d = vnorm(vadd(self->d, vscale(n, factor)));
     }
+    return w;
 }
 
 /* ------------------------------------------------------------------------- */
@@ -862,6 +879,76 @@ static int do_specular_reflection(ctx_t *c, const ray_t *ray, ray_t *next, float
     return hit;
 }
 
+/* get_direct_light_attenuation (path_tracer.rs:458-483): shadow segments toward the sampled sun
+ * direction until a miss or an opaque hit, attenuated by each hit's colour and alpha.  The
+ * segments share the path's next_intersection cap [C15]; a shadow ray that reaches it counts as
+ * occluded [C18]. */
+static void direct_light_attenuation(ctx_t *c, ray_t *r, float att[4], uint32_t *segs) {
+    att[0] = att[1] = att[2] = att[3] = 1.0f;
+    while (att[3] > 0.0f) {
+        if (c->path_segs >= MAX_PATH_SEGMENTS) { att[3] = 0.0f; break; } /* [C18] */
+        r->o = ray_at(r, RAY_OFFSET);
+        if (!next_intersection(c, r, segs)) break;
+        float mult = 1.0f - r->col[3];
+        for (int i = 0; i < 3; i++) att[i] *= r->col[i] * r->col[3] + mult;
+        att[3] *= mult;
+        if (c->sun.strict_direct_light &&
+            c->s->materials[r->prev_mat].ior != c->s->materials[r->cur_mat].ior)
+            att[3] = 0.0f;
+    }
+}
+
+/* Sun::get_random_sun_direction (scene/mod.rs:427-445): a cone of half-angle `radius` around sw;
+ * the result is (u + v) + normalize(w), not normalised, as written */
+static v3 random_sun_direction(const sun_k *k, uint32_t *rng) {
+    float x1 = ref_rng_next(rng), x2 = ref_rng_next(rng);
+    float cos_a = (1.0f - x1) + x1 * k->radius_cos;
+    float sin_a = sqrtf(1.0f - cos_a * cos_a);
+    float phi = 2.0f * PI_F * x2;
+    v3 u = vscale(k->su, ref_math_cos(phi) * sin_a);
+    v3 v = vscale(k->sv, ref_math_sin(phi) * sin_a);
+    v3 w = vscale(k->sw, cos_a);
+    return vadd(vadd(u, v), vnorm(w));
+}
+
+/* do_diffuse_reflection's sun-sampling branch (path_tracer.rs:225-291): next-event estimation
+ * toward the sun (presets FAST, HIGH_QUALITY), then the diffuse bounce.  ray.hit.color is read
+ * after diffuse_reflection, so its importance weights apply here (contrast [C5]). */
+static int diffuse_sun_sampling(ctx_t *c, ray_t *ray, ray_t *next, float cum[4], const ref_material *m,
+                                uint32_t *rng, fwd_t *fw, uint32_t *segs, const float emit[3], int hit) {
+    const sun_k *k = &c->sun;
+    float direct[3] = {0.0f, 0.0f, 0.0f};
+    int lit = 0;
+    new_from_self(ray, next);
+    next->d = random_sun_direction(k, rng);
+    int front_light = vdot(next->d, ray->n) > 0.0f;
+    if (front_light || ((m->flags & MAT_FLAG_SUBSURFACE) && ref_rng_next(rng) < c->s->f_sub_surface)) {
+        if (!front_light) next->o = vadd(next->o, vscale(ray->n, -RAY_OFFSET));
+        next->cur_mat = next->prev_mat;
+        float att[4];
+        direct_light_attenuation(c, next, att, segs);
+        if (att[3] > 0.0f) {
+            float mult = fabsf(vdot(next->d, ray->n)) * k->lum_a;
+            for (int i = 0; i < 3; i++) direct[i] = att[i] * att[3] * mult;
+            hit = 1;
+            lit = 1;
+        }
+    }
+    float wgt = diffuse_reflection(c, next, ray, rng);
+    for (int i = 0; i < 4; i++) ray->col[i] *= wgt;
+    if (fw) {
+        if (c->s->emitters_enabled && m->emittance > RAY_EPSILON)
+            for (int i = 0; i < 3; i++) fw->L[i] = fw->L[i] + fw->T[i] * emit[i];
+        for (int i = 0; i < 3; i++) fw->T[i] = fw->T[i] * ray->col[i];
+        if (lit) for (int i = 0; i < 3; i++) fw->L[i] = fw->L[i] + fw->T[i] * (direct[i] * k->emit[i]);
+    }
+    hit = path_trace(c, next, 0, rng, fw, segs) || hit;
+    if (hit)
+        for (int i = 0; i < 3; i++)
+            cum[i] += emit[i] + ray->col[i] * ((direct[i] * k->emit[i] + next->col[i]) + 0.0f);
+    return hit;
+}
+
 static int do_diffuse_reflection(ctx_t *c, ray_t *ray, ray_t *next, float cum[4], const ref_material *m,
                                  uint32_t *rng, fwd_t *fw, uint32_t *segs) { /* :190-316 */
     int hit = 0;
@@ -871,6 +958,7 @@ static int do_diffuse_reflection(ctx_t *c, ray_t *ray, ray_t *next, float cum[4]
         for (int i = 0; i < 3; i++) emit[i] = ray->col[i] * ray->col[i] * m->emittance;
         hit = 1;
     }
+    if (c->sun.sun_sampling) return diffuse_sun_sampling(c, ray, next, cum, m, rng, fw, segs, emit, hit);
     /* sun_sampling == false (IMPORTANCE preset) -> :292-314 */
     float ray_color[4];
     memcpy(ray_color, ray->col, sizeof ray_color);

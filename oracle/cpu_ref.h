@@ -59,6 +59,10 @@ typedef struct {
     float luminosity;
     uint8_t texture_rgba[4]; /* Sun texture is a Texture::Color */
     int32_t importance_sampling, diffuse_sun, sun_sampling;
+    /* SunSamplingStrategy::{strict_direct_light, sun_luminosity} (scene/mod.rs:66-67) and
+     * Sun::luminosity_pdf (:274, 376) -- the next-event-estimation presets FAST / HIGH_QUALITY */
+    int32_t strict_direct_light, sun_luminosity;
+    float luminosity_pdf;
 } ref_sun;
 
 typedef struct {
@@ -82,6 +86,7 @@ typedef struct {
     const uint8_t *texels;
     ref_sun sun;
     int32_t emitters_enabled;
+    float f_sub_surface; /* Scene::f_sub_surface (scene/mod.rs:152), path_tracer.rs:237-241 */
 } ref_scene;
 
 typedef struct {

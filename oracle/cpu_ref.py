@@ -41,7 +41,8 @@ class RefSun(C.Structure):
                 ("apparent_color", C.c_float * 3), ("draw_texture", C.c_int32), ("texture_modification", C.c_int32),
                 ("importance_sample_chance", C.c_float), ("importance_sample_radius", C.c_float),
                 ("luminosity", C.c_float), ("texture_rgba", C.c_uint8 * 4), ("importance_sampling", C.c_int32),
-                ("diffuse_sun", C.c_int32), ("sun_sampling", C.c_int32)]
+                ("diffuse_sun", C.c_int32), ("sun_sampling", C.c_int32), ("strict_direct_light", C.c_int32),
+                ("sun_luminosity", C.c_int32), ("luminosity_pdf", C.c_float)]
 
 
 class RefScene(C.Structure):
@@ -51,7 +52,8 @@ class RefScene(C.Structure):
                 ("sphere_material", C.c_void_p), ("n_spheres", C.c_uint32), ("cuboids", C.c_void_p),
                 ("cuboid_material", C.c_void_p), ("n_cuboids", C.c_uint32), ("materials", C.c_void_p),
                 ("n_materials", C.c_uint32), ("textures", C.c_void_p), ("n_textures", C.c_uint32),
-                ("texels", C.c_void_p), ("sun", RefSun), ("emitters_enabled", C.c_int32)]
+                ("texels", C.c_void_p), ("sun", RefSun), ("emitters_enabled", C.c_int32),
+                ("f_sub_surface", C.c_float)]
 
 
 class RefParams(C.Structure):
@@ -197,10 +199,12 @@ class OracleScene:
         sun = RefSun(s.azimuth, s.altitude, s.radius, (C.c_float * 4)(*s.color), (C.c_float * 3)(*s.apparent_color),
                      int(s.draw_texture), int(s.texture_modification), s.importance_sample_chance,
                      s.importance_sample_radius, s.luminosity, (C.c_uint8 * 4)(*s.texture_rgba),
-                     int(st.importance_sampling), int(st.diffuse_sun), int(st.sun_sampling))
+                     int(st.importance_sampling), int(st.diffuse_sun), int(st.sun_sampling),
+                     int(st.strict_direct_light), int(st.sun_luminosity), s.luminosity_pdf)
         self.s = RefScene(_p(mask), _p(ch), len(mask), t.root, t.depth, _p(lf), _p(lc), _p(lp), len(lf), _p(sp), _p(sm),
                           len(sp), _p(cb), _p(cm), len(cb), C.cast(mats, C.c_void_p), len(scene.materials),
-                          C.cast(texs, C.c_void_p), len(scene.textures), _p(texels), sun, int(scene.emitters_enabled))
+                          C.cast(texs, C.c_void_p), len(scene.textures), _p(texels), sun, int(scene.emitters_enabled),
+                          scene.f_sub_surface)
 
 
 def render(scene, camera, width, height, spp, *, spp_start=0, max_depth=5, seed=1, threads=8, forward=False,

@@ -32,6 +32,11 @@ RENDERS = {
     "c3_small": ("C3", 96, 54, 2, None),
     "c4_small": ("C4", 64, 36, 2, None),  # cuboids + image textures (procedural, scene.py)
     "c5_small": ("C5", 96, 54, 2, None),  # 1 M unit-block voxel terrain, depth 11
+    # sun sampling (next-event estimation): config + scene.SUN_VARIANTS entry
+    "tiny_fast": ("tiny", 64, 48, 4, None, "fast"),
+    "c2_hq": ("C2", 160, 90, 2, None, "hq"),
+    "c4_hq_sss": ("C4", 64, 36, 2, None, "hq_sss"),
+    "c5_nee_importance": ("C5", 96, 54, 2, None, "nee_importance"),
 }
 # RendererMode::Preview fixtures: name -> (config, width, height)
 PREVIEWS = {
@@ -42,13 +47,16 @@ PREVIEWS = {
 
 
 def render_fixture(name):
-    cfg, W, H, spp, md = RENDERS[name]
+    cfg, W, H, spp, md, *variant = RENDERS[name]
     sc, cam, rs = S.make_config(cfg)
+    if variant:
+        S.with_sun_variant(sc, variant[0])
     acc, seg, st = cpu_ref.render(sc, cam, W, H, spp, max_depth=md or rs.max_depth, seed=rs.seed, forward=True,
                                   threads=8)
     return dict(accum=acc, segcount=seg, stats=np.array([st[k] for k in STAT_KEYS], np.uint64),
                 meta=np.array(json.dumps(dict(config=cfg, width=W, height=H, spp=spp,
-                                              max_depth=md or rs.max_depth, seed=rs.seed, forward=True))))
+                                              max_depth=md or rs.max_depth, seed=rs.seed, forward=True,
+                                              **(dict(sun_variant=variant[0]) if variant else {})))))
 
 
 def preview_fixture(name):

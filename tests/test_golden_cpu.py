@@ -12,7 +12,7 @@ from octree_pathtracing_amd import scene as S
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
 RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c5_small", "c3_preview", "c4_preview",
-           "c5_preview"]
+           "c5_preview", "tiny_fast", "c2_hq", "c4_hq_sss", "c5_nee_importance"]
 STAT_KEYS = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
              "texel_reads", "max_path_segs")
 
@@ -26,6 +26,8 @@ def test_oracle_reproduces_render_fixture(name):
     g = load(name)
     m = json.loads(str(g["meta"]))
     sc, cam, _ = S.make_config(m["config"])
+    if "sun_variant" in m:
+        S.with_sun_variant(sc, m["sun_variant"])
     acc, seg, st = cpu_ref.render(sc, cam, m["width"], m["height"], m["spp"], max_depth=m["max_depth"],
                                   seed=m["seed"], forward=m["forward"], threads=8, preview=m.get("preview", False))
     assert np.array_equal(seg, g["segcount"])

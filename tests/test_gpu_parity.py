@@ -229,11 +229,6 @@ def test_validation_errors(renderer):
     with pytest.raises(_lib.OctptError) as e:
         renderer.set_scene(bad)
     assert e.value.status == _lib.ERR_INVALID_ARG
-    nee = S.make_config("tiny")[0]
-    nee.strategy = S.STRATEGY_HIGH_QUALITY
-    with pytest.raises(_lib.OctptError) as e:
-        renderer.set_scene(nee)
-    assert e.value.status == _lib.ERR_UNSUPPORTED
     renderer.set_scene(sc)
     p = renderer.params(rs.width, rs.height, 0, 1)
     p.branch_count = 10
@@ -357,7 +352,8 @@ GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
 
 
 @pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c5_small",
-                                  "c3_preview", "c4_preview", "c5_preview"])
+                                  "c3_preview", "c4_preview", "c5_preview", "tiny_fast", "c2_hq", "c4_hq_sss",
+                                  "c5_nee_importance"])
 def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     """GPU render vs the committed oracle fixture (tests/golden/make_golden.py): exact per-pixel
     segment counts and work totals, radiance within REL_TOL_FORWARD."""
@@ -368,6 +364,8 @@ def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     g = np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
     m = json.loads(str(g["meta"]))
     sc, cam, rs = S.make_config(m["config"])
+    if "sun_variant" in m:
+        S.with_sun_variant(sc, m["sun_variant"])
     rs.width, rs.height, rs.spp, rs.max_depth, rs.seed = m["width"], m["height"], m["spp"], m["max_depth"], m["seed"]
     acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs, preview=m.get("preview", False))
     keys = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
@@ -484,3 +482,51 @@ def test_renderer_preview_mode(renderer):
         assert np.array_equal(renderer.get_float_image(), ref)
     finally:
         renderer.set_mode(RendererMode.PathTraced)
+
+
+# ---------------------------------------------------------------------------------------------
+# sun sampling (next-event estimation): shadow segments between a diffuse hit and
+# its bounce, through the kNee shade / megakernel instances
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name,variant,res", [("tiny", "fast", None), ("tiny", "hq_sss", None),
+                                              ("C2", "hq", (160, 90, 4)), ("C3", "fast", (192, 108, 2)),
+                                              ("C4", "hq_sss", (128, 72, 2)), ("C5", "nee_importance", (192, 108, 2))])
+def test_sun_sampling_parity(torch_cuda, renderer, name, variant, res):
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config(name)
+    S.with_sun_variant(sc, variant)
+    if res:
+        rs.width, rs.height, rs.spp = res
+    gpu = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    ref = oracle(sc, cam, rs, forward=True)
+    exact = assert_parity(gpu, ref, f"{name}/{variant}")
+    assert exact > 0.999, f"{name}/{variant}: only {exact:.4%} of channels bit-identical"
+    rec = oracle(sc, cam, rs, forward=False)
+    assert rel_err(gpu[0], rec[0]).max() <= REL_TOL_RECURSIVE
+
+
+@pytest.mark.parametrize("variant", ["fast", "hq_sss"])
+def test_sun_sampling_megakernel_and_small_pool(torch_cuda, renderer, variant):
+    """The megakernel keeps the waiting bounce in registers, the wavefront in the slot's NEE planes:
+    both bit-identical, also when slots are recycled across 3 chunks with a 100-path pool."""
+    import os
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    sc, cam, rs = S.make_config("tiny")
+    S.with_sun_variant(sc, variant)
+    rs.width, rs.height, rs.spp = 37, 19, 6
+    a = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    b = gpu_render(torch_cuda, renderer, sc, cam, rs, megakernel=True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    os.environ["OCTPT_POOL"] = "100"
+    os.environ["OCTPT_REFILL"] = "1"
+    os.environ["OCTPT_CHUNK"] = "2000"
+    try:
+        small = HipRenderer(0)
+        c = gpu_render(torch_cuda, small, sc, cam, rs)
+        small.close()
+    finally:
+        del os.environ["OCTPT_POOL"], os.environ["OCTPT_REFILL"], os.environ["OCTPT_CHUNK"]
+    assert np.array_equal(a[0], c[0]) and np.array_equal(a[1], c[1])
