@@ -69,6 +69,32 @@ typedef struct octpt_cuboid {
     uint32_t face_material[6];
 } octpt_cuboid;
 
+/* Block models.  A leaf cuboid whose cuboid_model entry is not
+ * OCTPT_MODEL_NONE is a Minecraft block-model instance (the reference's ResourceModel::Quad leaf,
+ * octree_traversal.rs:207-213; Scene::quads, scene/mod.rs:153): its box is the voxel [min, min+1)
+ * and its surface is the model's quads, tested with Quad::hit (src/geometry/quad.rs:172-200) in
+ * voxel-local coordinates, instead of the six faces of the box.
+ * geometry::quad::Quad::new arguments (quad.rs:90-114): origin, edge vectors u and v (voxel-local,
+ * the block is [0,1]^3), texture u/v ranges (the face's uv rectangle / 16) and the material.
+ * The plane, normal and w = n / (n.n) are derived at upload exactly as Quad::new does.  64 bytes. */
+typedef struct octpt_quad {
+    float origin[3];
+    uint32_t material;
+    float u[3];
+    float v[3];
+    float texture_u_range[2];
+    float texture_v_range[2];
+    uint32_t reserved[2];
+} octpt_quad;
+/* gpu_structs::model::Model (src/gpu_structs/model.rs:14-21): the model's quads are
+ * quads[first_quad .. first_quad + quad_count).  16 bytes. */
+typedef struct octpt_block_model {
+    uint32_t flags; /* reserved, 0 */
+    uint32_t first_quad, quad_count;
+    uint32_t reserved;
+} octpt_block_model;
+#define OCTPT_MODEL_NONE 0xFFFFFFFFu
+
 /* GPUMaterial (src/gpu_structs/gpu_material.rs:67-76), 32 bytes */
 typedef struct octpt_material {
     float ior, specular, emittance, roughness, metalness;
@@ -123,6 +149,13 @@ typedef struct octpt_scene_desc {
     octpt_sun sun;
     int32_t emitters_enabled;
     float f_sub_surface; /* Scene::f_sub_surface (scene/mod.rs:152): subsurface sun-sample chance */
+    /* block models (C19): cuboid_model (nullable = no models) holds one entry per cuboid,
+     * OCTPT_MODEL_NONE for a plain box or a model index; such a cuboid must be a unit voxel */
+    const uint32_t *cuboid_model;
+    const octpt_block_model *models;
+    uint32_t model_count;
+    const octpt_quad *quads;
+    uint32_t quad_count;
 } octpt_scene_desc;
 
 /* renderer::camera::Camera (src/renderer/camera.rs:8-25) */

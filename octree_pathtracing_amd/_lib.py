@@ -67,6 +67,24 @@ class Cuboid(C.Structure):
     _fields_ = [("min", C.c_float * 3), ("max", C.c_float * 3), ("face_material", C.c_uint32 * 6)]
 
 
+class Quad(C.Structure):
+    """octpt_quad: Quad::new arguments (quad.rs:90-114), voxel-local (DESIGN.md C19)."""
+    _fields_ = [("origin", C.c_float * 3), ("material", C.c_uint32), ("u", C.c_float * 3), ("v", C.c_float * 3),
+                ("texture_u_range", C.c_float * 2), ("texture_v_range", C.c_float * 2), ("reserved", C.c_uint32 * 2)]
+
+
+class BlockModel(C.Structure):
+    """octpt_block_model (gpu_structs/model.rs:14-21)."""
+    _fields_ = [("flags", C.c_uint32), ("first_quad", C.c_uint32), ("quad_count", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+MODEL_NONE = 0xFFFFFFFF
+# numpy view of octpt_quad rows (Scene.quads)
+QUAD_DTYPE = [("origin", "<f4", (3,)), ("material", "<u4"), ("u", "<f4", (3,)), ("v", "<f4", (3,)),
+              ("texture_u_range", "<f4", (2,)), ("texture_v_range", "<f4", (2,)), ("reserved", "<u4", (2,))]
+
+
 class Material(C.Structure):
     _fields_ = [
         ("ior", C.c_float), ("specular", C.c_float), ("emittance", C.c_float), ("roughness", C.c_float),
@@ -98,6 +116,8 @@ class SceneDesc(C.Structure):
         ("spheres", C.c_void_p), ("sphere_count", C.c_uint32), ("cuboids", C.c_void_p), ("cuboid_count", C.c_uint32),
         ("materials", C.c_void_p), ("material_count", C.c_uint32), ("textures", C.c_void_p),
         ("texture_count", C.c_uint32), ("sun", Sun), ("emitters_enabled", C.c_int32), ("f_sub_surface", C.c_float),
+        ("cuboid_model", C.c_void_p), ("models", C.c_void_p), ("model_count", C.c_uint32), ("quads", C.c_void_p),
+        ("quad_count", C.c_uint32),
     ]
 
 

@@ -83,7 +83,7 @@ struct octpt_ctx {
     float build_ms = 0.0f;  // device time of the last octpt_build_octree_device
     BuildScratch build_scratch;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
-    int extend_bpc_cache[kMaxDepth + 1][2][3] = {};
+    int extend_bpc_cache[kMaxDepth + 1][3][3] = {};  // [depth][kPrims][variant]
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
     size_t pool = 0, color_cap = 0;
@@ -241,6 +241,28 @@ int subtree_height(const octpt_scene_desc &d, uint32_t node, std::vector<int8_t>
     return best;
 }
 
+// Quad::new (quad.rs:90-114): n = u x v, normal = n * (1 / |n|), w = n / (n . n), d = normal . origin
+DevQuad make_dev_quad(const octpt_quad &x) {
+    const float *u = x.u, *v = x.v, *o = x.origin;
+    const float n[3] = {u[1] * v[2] - v[1] * u[2], u[2] * v[0] - v[2] * u[0], u[0] * v[1] - v[0] * u[1]};
+    const float nn = (n[0] * n[0] + n[1] * n[1]) + n[2] * n[2];
+    const float r = 1.0f / sqrtf(nn);
+    const float nrm[3] = {n[0] * r, n[1] * r, n[2] * r};
+    const float dd = (nrm[0] * o[0] + nrm[1] * o[1]) + nrm[2] * o[2];
+    DevQuad q{};
+    uint32_t mb;
+    std::memcpy(&mb, &x.material, 4);
+    float mat;
+    std::memcpy(&mat, &mb, 4);
+    q.o_d = make_float4(o[0], o[1], o[2], dd);
+    q.u_mat = make_float4(u[0], u[1], u[2], mat);
+    q.v_tu0 = make_float4(v[0], v[1], v[2], x.texture_u_range[0]);
+    q.w_tu1 = make_float4(n[0] / nn, n[1] / nn, n[2] / nn, x.texture_u_range[1]);
+    q.n_tv0 = make_float4(nrm[0], nrm[1], nrm[2], x.texture_v_range[0]);
+    q.tv1 = make_float4(x.texture_v_range[1], 0.0f, 0.0f, 0.0f);
+    return q;
+}
+
 octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d) {
     if (!d) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene is NULL");
     if (d->abi_version != OCTPT_ABI_VERSION) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene abi_version mismatch");
@@ -288,6 +310,27 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d) {
         for (int f = 0; f < 6; ++f)
             if (d->cuboids[c].face_material[f] >= d->material_count)
                 return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboid material out of range");
+    // block models (C19)
+    if (d->cuboid_model) {
+        if (d->model_count && !d->models) return fail(ctx, OCTPT_ERR_INVALID_ARG, "models is NULL");
+        if (d->quad_count && !d->quads) return fail(ctx, OCTPT_ERR_INVALID_ARG, "quads is NULL");
+        if (d->quad_count >= kQuadKey) return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^30 - 1 quads");
+        for (uint32_t c = 0; c < d->cuboid_count; ++c) {
+            const uint32_t m = d->cuboid_model[c];
+            if (m == OCTPT_MODEL_NONE) continue;
+            if (m >= d->model_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboid model index out of range");
+            const octpt_cuboid &b = d->cuboids[c];
+            for (int a = 0; a < 3; ++a)
+                if (b.max[a] != b.min[a] + 1.0f)
+                    return fail(ctx, OCTPT_ERR_INVALID_ARG, "a block-model cuboid must be a unit voxel [min, min+1)");
+        }
+        for (uint32_t m = 0; m < d->model_count; ++m)
+            if ((uint64_t)d->models[m].first_quad + d->models[m].quad_count > d->quad_count)
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "model quad range exceeds quads");
+        for (uint32_t q = 0; q < d->quad_count; ++q)
+            if (d->quads[q].material >= d->material_count)
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "quad material out of range");
+    }
     for (uint32_t m = 0; m < d->material_count; ++m)
         if (d->materials[m].texture_index >= d->texture_count)
             return fail(ctx, OCTPT_ERR_INVALID_ARG, "material texture_index out of range");
@@ -450,7 +493,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
     octpt_status st = ensure_wave(ctx, pool, chunk_max);
     if (st != OCTPT_OK) return st;
-    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_cuboids ? 1 : 0][ctx->leaf_batch == kLeafSplit ? 2 : (ctx->leaf_batch ? 1 : 0)];
+    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)][ctx->leaf_batch == kLeafSplit ? 2 : (ctx->leaf_batch ? 1 : 0)];
     if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S, ctx->leaf_batch);
     const int grid_extend = ctx->num_cu * bpc;
     if (std::getenv("OCTPT_DEBUG"))
@@ -763,6 +806,18 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
             cmax[c] = make_float2(x.max[1], x.max[2]);
             std::memcpy(&cmat[(size_t)c * 6], x.face_material, 24);
         }
+        // block models (C19): Quad::new (quad.rs:90-114) in glam's f32 operation order
+        bool has_models = false;
+        if (d->cuboid_model)
+            for (uint32_t c = 0; c < d->cuboid_count && !has_models; ++c) has_models = d->cuboid_model[c] != OCTPT_MODEL_NONE;
+        std::vector<DevQuad> quads;
+        std::vector<uint2> models;
+        if (has_models) {
+            quads.resize(d->quad_count);
+            for (uint32_t q = 0; q < d->quad_count; ++q) quads[q] = make_dev_quad(d->quads[q]);
+            models.resize(d->model_count);
+            for (uint32_t m = 0; m < d->model_count; ++m) models[m] = make_uint2(d->models[m].first_quad, d->models[m].quad_count);
+        }
         float lf[256];
         uint8_t lb[256];
         make_luts(lf, lb);
@@ -819,6 +874,14 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         HIP_TRY(ctx, upload(ctx, mats.data(), mats.size(), &d_mats));
         HIP_TRY(ctx, upload(ctx, texs.data(), texs.size(), &d_texs));
         HIP_TRY(ctx, upload(ctx, texels.data(), texels.size(), &d_texels));
+        uint32_t *d_cmodel = nullptr;
+        uint2 *d_models = nullptr;
+        DevQuad *d_quads = nullptr;
+        if (has_models) {
+            HIP_TRY(ctx, upload(ctx, d->cuboid_model, d->cuboid_count, &d_cmodel));
+            HIP_TRY(ctx, upload(ctx, models.data(), models.size(), &d_models));
+            HIP_TRY(ctx, upload(ctx, quads.data(), quads.size(), &d_quads));
+        }
         S.node_child = d_child;
         S.root = base[d->root];  // traversal "parent" values are child-array bases
         S.root_mask = d->octants[d->root].child_mask;
@@ -834,6 +897,10 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.cub_a = d_cmin;
         S.cub_b = d_cmax;
         S.cub_mat = d_cmat;
+        S.cub_model = d_cmodel;
+        S.models = d_models;
+        S.quads = d_quads;
+        S.has_models = has_models ? 1u : 0u;
         S.mats = d_mats;
         S.texs = d_texs;
         S.texels = d_texels;

@@ -59,6 +59,22 @@ struct DevSun {
     float f_sub_surface;  // Scene::f_sub_surface
 };
 
+// block-model quad: Quad::new's derived plane, normal and w (quad.rs:90-114), 96 B
+struct alignas(16) DevQuad {
+    float4 o_d;    // (origin.xyz, d = normal . origin)
+    float4 u_mat;  // (u.xyz, material bits)
+    float4 v_tu0;  // (v.xyz, texture_u_range.x)
+    float4 w_tu1;  // (w.xyz = n / (n . n), texture_u_range.y)
+    float4 n_tv0;  // (normal.xyz, texture_v_range.x)
+    float4 tv1;    // (texture_v_range.y, 0, 0, 0)
+};
+
+// primitive kinds a kernel instance handles (wf_extend_kernel's kPrims)
+constexpr int kPrimsSpheres = 0, kPrimsBoxes = 1, kPrimsModels = 2;
+// self-intersection key of a ray leaving quad q: kQuadKey | q; prim ids are
+// sphere indices < 2^27 or kPrimCuboidBit | index, so the keys never collide
+constexpr uint32_t kQuadKey = 0x40000000u;
+
 struct DevScene {
     // sparse packed child slots: an octant's present children are contiguous from
     // its base; octant child = (its base, its child_mask), leaf child = (prim id, 1) or
@@ -74,6 +90,10 @@ struct DevScene {
     const float4 *cub_a;            // (min.x, min.y, min.z, max.x)
     const float2 *cub_b;            // (max.y, max.z): 24 B per box in two loads, no padding lanes
     const uint32_t *cub_mat;        // 6 per cuboid
+    const uint32_t *cub_model;      // per cuboid: OCTPT_MODEL_NONE or a block model (C19); has_models only
+    const uint2 *models;            // (first quad, quad count)
+    const DevQuad *quads;
+    uint32_t has_models;
     const DevMaterial *mats;
     const DevTexture *texs;
     const uint8_t *texels;

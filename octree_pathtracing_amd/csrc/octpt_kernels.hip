@@ -326,6 +326,49 @@ __device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const Trac
     return true;
 }
 
+// Quad::hit (geometry/quad.rs:172-200) in voxel-local coordinates, with the plane, normal and w
+// derived at upload as Quad::new does (:90-114).  Accepts 0 < t <= t_next (back faces culled).
+__device__ __forceinline__ bool quad_hit(const DevQuad &Q, v3 o_local, v3 d, float t_next, float &t, float &alpha,
+                                         float &beta) {
+    const float4 a = Q.o_d, n4 = Q.n_tv0;
+    const v3 nrm = V(n4.x, n4.y, n4.z);
+    const float denom = vdot(d, nrm);
+    if (denom >= -RAY_EPSILON) return false;
+    t = (a.w - vdot(nrm, o_local)) / denom;
+    if (t <= 0.0f || t > t_next) return false;
+    const float4 u4 = Q.u_mat, v4 = Q.v_tu0, w4 = Q.w_tu1;
+    const v3 qu = V(u4.x, u4.y, u4.z), qv = V(v4.x, v4.y, v4.z), qw = V(w4.x, w4.y, w4.z);
+    const v3 planar = vsub(vadd(o_local, vscale(d, t)), V(a.x, a.y, a.z));
+    alpha = vdot(qw, vcross(planar, qv));
+    beta = vdot(qw, vcross(qu, planar));
+    return alpha >= 0.0f && alpha <= 1.0f && beta >= 0.0f && beta <= 1.0f;
+}
+
+// a block-model leaf (the reference's ResourceModel::Quad arm, octree_traversal.rs:207-213) [C19]:
+// the closest of the model's quads with 0 < t <= t_accept, ties to the later quad (Quad::hit's
+// `t > t_next` test), skipping the quad the ray leaves (last_prim = kQuadKey | quad)
+__device__ inline bool model_test(const DevScene &S, const TraceRay &r, v3 voxel, uint32_t mdl, float t_accept,
+                                  float &t_best, uint32_t &q_best, float &al_best, float &be_best) {
+    const uint2 m = S.models[mdl];
+    const v3 ol = vsub(r.o, voxel);
+    float t_next = t_accept;
+    bool found = false;
+    for (uint32_t k = 0; k < m.y; ++k) {
+        const uint32_t q = m.x + k;
+        if ((kQuadKey | q) == r.last_prim) continue;
+        float t, al, be;
+        if (quad_hit(S.quads[q], ol, r.d, t_next, t, al, be)) {
+            t_next = t;
+            q_best = q;
+            al_best = al;
+            be_best = be;
+            found = true;
+        }
+    }
+    t_best = t_next;
+    return found;
+}
+
 __device__ __forceinline__ uint32_t face_index(uint32_t axis, float sgn) {
     if (axis == 0u) return sgn < 0.0f ? 0u : 1u;
     if (axis == 1u) return sgn < 0.0f ? 2u : 3u;
@@ -344,6 +387,27 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
         n = V((p.x - sp.x) / sp.w, (p.y - sp.y) / sp.w, (p.z - sp.z) / sp.w);
         mat = S.sphere_mat[prim];
         uv_ready = false;  // sphere uv only feeds image textures (computed lazily below)
+    } else if (S.has_models && S.cub_model[prim & ~kPrimCuboidBit] != OCTPT_MODEL_NONE) {
+        // block-model hit [C19]: the hit record holds the instance and t; the quad is the one
+        // model_test chose, found again by the same computation with t_next = t
+        const uint32_t ci = prim & ~kPrimCuboidBit;
+        const float4 ca = S.cub_a[ci];
+        uint32_t q = 0u;
+        float al = 0.0f, be = 0.0f, tq;
+        TraceRay tr;
+        tr.o = r.o;
+        tr.d = r.d;
+        tr.last_prim = r.last_prim;
+        tr.self_inward = false;
+        model_test(S, tr, V(ca.x, ca.y, ca.z), S.cub_model[ci], h.t, tq, q, al, be);
+        const DevQuad &Q = S.quads[q];
+        n = V(Q.n_tv0.x, Q.n_tv0.y, Q.n_tv0.z);
+        mat = __float_as_uint(Q.u_mat.w);
+        const float tu0 = Q.v_tu0.w, tu1 = Q.w_tu1.w, tv0 = Q.n_tv0.w, tv1 = Q.tv1.x;
+        u = tu0 + al * (tu1 - tu0);  // quad.rs:194-197
+        v = tv0 + be * (tv1 - tv0);
+        uv_ready = true;
+        prim = kQuadKey | q;  // the self-intersection key of the next segment
     } else {
         const uint32_t ci = prim & ~kPrimCuboidBit;
         const float4 ca = S.cub_a[ci];
@@ -459,22 +523,33 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 
+
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
 // common single-primitive leaf (one dependent load fewer).  t_accept = t_exit_w + CELL_TOL * cell_w.
-// kCuboids = false: sphere-only scenes; the slab test's temporaries then never reserve
-// registers (71 instead of 85 VGPRs in wf_extend_kernel: 7 waves/SIMD instead of 5).
-template <bool kCuboids>
+// kPrims: the primitive kinds a scene holds (kPrimsSpheres: the slab test's temporaries never
+// reserve registers, 7 waves/SIMD in wf_extend_kernel; kPrimsBoxes adds cuboids, kPrimsModels
+// block-model cuboids)
+template <int kPrims>
 __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, uint32_t prim, v3 inv, float t_accept,
                                           PrimHit &h, Counters &cnt) {
     const bool self_prim = prim == r.last_prim;
     bool ok;
-    if (!kCuboids || !(prim & kPrimCuboidBit)) {
+    if (kPrims == kPrimsSpheres || !(prim & kPrimCuboidBit)) {
         cnt.sph++;
         ok = sphere_test(S.spheres[prim], r, self_prim, h);
     } else {
         cnt.cub++;
         const uint32_t ci = prim & ~kPrimCuboidBit;
         const float4 ca = S.cub_a[ci];
+        if (kPrims == kPrimsModels && S.has_models) {
+            const uint32_t mdl = S.cub_model[ci];
+            if (mdl != OCTPT_MODEL_NONE) {
+                uint32_t q;
+                float al, be;
+                h.f = 0u;
+                return model_test(S, r, V(ca.x, ca.y, ca.z), mdl, t_accept, h.t, q, al, be);
+            }
+        }
         const float2 cb = S.cub_b[ci];
         ok = cuboid_test(make_float4(ca.x, ca.y, ca.z, 0.0f), make_float4(ca.w, cb.x, cb.y, 0.0f), r, inv, self_prim, h);
     }
@@ -485,20 +560,20 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
 // registers (70 instead of 85 VGPRs in wf_extend_kernel: 7 waves/SIMD instead of 5).
 // The first primitive is tested straight-line (leaves hold 1.02 primitives on average); the
 // rest of a multi-primitive list in a loop, keeping the closest accepted hit.
-template <bool kCuboids = true>
+template <int kPrims = kPrimsModels>
 __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt) {
     // three correctly-rounded divides: only scenes holding cuboids pay for them (uniform branch)
     v3 inv = V(0.0f, 0.0f, 0.0f);
-    if (kCuboids && S.has_cuboids) inv = ray_inv_dir(r.d);
+    if (kPrims != kPrimsSpheres && S.has_cuboids) inv = ray_inv_dir(r.d);
     uint32_t prim = lr.x;
     if (lr.y != 1u) prim = S.leaf_prims[lr.x];
-    bool found = prim_test<kCuboids>(S, r, prim, inv, t_accept, best, cnt);
+    bool found = prim_test<kPrims>(S, r, prim, inv, t_accept, best, cnt);
     if (found) best_prim = prim;
     for (uint32_t k = 1; k < lr.y; ++k) {
         const uint32_t p = S.leaf_prims[lr.x + k];
         PrimHit hk;
-        if (prim_test<kCuboids>(S, r, p, inv, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
+        if (prim_test<kPrims>(S, r, p, inv, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
             best = hk;
             best_prim = p;
             found = true;
@@ -513,7 +588,7 @@ enum : int { kStepLeaf = 3 };
 // not tested here -- the step returns kStepLeaf with (leaf, t_accept) and E.resume set; the caller
 // tests the leaf later (wave-batched) and, on a miss, calls esvo_step again, which then performs
 // the same iteration's advance without counting the iteration twice (octree_traversal.rs:142-260).
-template <bool kDefer, bool kCuboids = true, uint32_t kS = kBlock>
+template <bool kDefer, int kPrims = kPrimsModels, uint32_t kS = kBlock>
 __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk, Counters &cnt,
                                 uint32_t &prim, PrimHit &h, uint2 &leaf, float &t_accept) {
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
@@ -548,7 +623,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
             E.resume = true;
             return kStepLeaf;
         }
-        if (leaf_test<kCuboids>(S, ray, slot, t_accept, prim, h, cnt)) return kStepHit;
+        if (leaf_test<kPrims>(S, ray, slot, t_accept, prim, h, cnt)) return kStepHit;
     }
     // Descend (:216-244) and advance (:249-260) as one select-based update: every lane computes
     // X = t_coef * f + t_corner with f = half for descend (X = t_center) and f = 0 otherwise
@@ -1331,7 +1406,7 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #ifndef OCTPT_EXTEND_WAVES
 #define OCTPT_EXTEND_WAVES 1
 #endif
-template <bool kDefer, bool kCuboids>
+template <bool kDefer, int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            uint32_t leaf_batch, unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
@@ -1391,7 +1466,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
                 pend = false;
                 uint32_t prim = kPrimNone;
                 PrimHit h;
-                if (leaf_test<kCuboids>(S, tr, leaf, t_accept, prim, h, cnt)) {
+                if (leaf_test<kPrims>(S, tr, leaf, t_accept, prim, h, cnt)) {
                     B.hit[pos] = hit_record(prim, h);
                     cnt.steps += E.iter;
                     active = false;
@@ -1401,7 +1476,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
         if (active && !pend) {
             uint32_t prim = kPrimNone;
             PrimHit h;
-            const int rs = esvo_step<kDefer, kCuboids>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
+            const int rs = esvo_step<kDefer, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
             if (rs == kStepLeaf) {
                 pend = true;
             } else if (rs != kStepContinue) {
@@ -1438,7 +1513,7 @@ __host__ __device__ __forceinline__ size_t split_stack_bytes(uint32_t depth) {
     return ((size_t)(depth - 1u) * kTravLanes * (sizeof(uint2) + sizeof(uint16_t)) + 15u) & ~(size_t)15u;
 }
 
-template <bool kCuboids>
+template <int kPrims>
 __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                                  uint32_t unused, unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
@@ -1487,7 +1562,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
                                                    (__float_as_uint(r1.w) >> 31) != 0u);
                 uint32_t prim = kPrimNone;
                 PrimHit h;
-                const bool found = leaf_test<kCuboids>(S, tr, slot, t_accept, prim, h, cnt);
+                const bool found = leaf_test<kPrims>(S, tr, slot, t_accept, prim, h, cnt);
                 jobs[j].prim = found ? prim : kPrimNone;
                 jobs[j].t = h.t;
                 jobs[j].flags = h.f & 15u;
@@ -1556,7 +1631,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
             if (active && !pend) {
                 uint32_t prim = kPrimNone;
                 PrimHit h;
-                const int rs = esvo_step<true, kCuboids>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
+                const int rs = esvo_step<true, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
                 if (rs == kStepLeaf) {
                     jobs[tid].pos = pos;
                     jobs[tid].lx = leaf.x;
@@ -1744,13 +1819,16 @@ int render_blocks_per_cu(uint32_t depth) {
 // leaf_batch: 0 inline leaf tests, 1..64 wave-local deferral, kLeafSplit the wave-specialised kernel
 static const void *extend_instance(const DevScene &S, uint32_t leaf_batch) {
     if (leaf_batch == kLeafSplit)
-        return S.has_cuboids ? reinterpret_cast<const void *>(wf_extend_split_kernel<true>)
-                             : reinterpret_cast<const void *>(wf_extend_split_kernel<false>);
+        return S.has_cuboids ? reinterpret_cast<const void *>(wf_extend_split_kernel<kPrimsModels>)
+                             : reinterpret_cast<const void *>(wf_extend_split_kernel<kPrimsSpheres>);
+    if (S.has_models)
+        return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, kPrimsModels>)
+                          : reinterpret_cast<const void *>(wf_extend_kernel<false, kPrimsModels>);
     if (S.has_cuboids)
-        return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, true>)
-                          : reinterpret_cast<const void *>(wf_extend_kernel<false, true>);
-    return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, false>)
-                      : reinterpret_cast<const void *>(wf_extend_kernel<false, false>);
+        return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, kPrimsBoxes>)
+                          : reinterpret_cast<const void *>(wf_extend_kernel<false, kPrimsBoxes>);
+    return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, kPrimsSpheres>)
+                      : reinterpret_cast<const void *>(wf_extend_kernel<false, kPrimsSpheres>);
 }
 
 static size_t extend_lds_bytes(const DevScene &S, uint32_t leaf_batch) {

@@ -192,7 +192,9 @@ class Octree:
 
 @dataclass
 class Scene:
-    """scene::Scene (scene/mod.rs:146-156) with a primitive world in place of quads."""
+    """scene::Scene (scene/mod.rs:146-156): spheres and cuboids, plus block models (DESIGN.md C19):
+    a cuboid whose cuboid_model entry is not MODEL_NONE is a block-model instance whose surface is
+    the model's quads (Scene::quads, scene/mod.rs:153), as the reference's ResourceModel::Quad leaf."""
     spheres: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), F32))          # cx, cy, cz, r
     sphere_material: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
     cuboids: np.ndarray = field(default_factory=lambda: np.zeros((0, 6), F32))          # min xyz, max xyz
@@ -202,6 +204,9 @@ class Scene:
     sun: Sun = field(default_factory=Sun)
     strategy: SunSamplingStrategy = field(default_factory=lambda: STRATEGY_IMPORTANCE)
     emitters_enabled: bool = True
+    cuboid_model: np.ndarray | None = None   # u32 per cuboid, _lib.MODEL_NONE = plain box
+    models: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.uint32))   # first quad, count
+    quads: np.ndarray = field(default_factory=lambda: np.zeros(0, _lib.QUAD_DTYPE))
     f_sub_surface: float = 0.3  # Scene::f_sub_surface (scene/mod.rs:152), used by sun sampling (path_tracer.rs:240)
     octree: Octree | None = None
 
@@ -322,6 +327,16 @@ class Scene:
         desc.sun = self.sun_struct()
         desc.emitters_enabled = int(self.emitters_enabled)
         desc.f_sub_surface = self.f_sub_surface
+        if self.cuboid_model is not None and len(self.cuboids):
+            cmod = np.ascontiguousarray(self.cuboid_model, np.uint32)
+            mdl = np.zeros((max(len(self.models), 1), 4), np.uint32)
+            mdl[: len(self.models), 1:3] = np.asarray(self.models, np.uint32).reshape(-1, 2)
+            qd = np.ascontiguousarray(self.quads)
+            desc.cuboid_model = ptr(cmod)
+            desc.models = ptr(mdl)
+            desc.model_count = len(self.models)
+            desc.quads = ptr(qd) if len(qd) else None
+            desc.quad_count = len(qd)
         keep.extend([octs, mats, texs])
         return desc, keep
 
@@ -475,13 +490,8 @@ def block_tile(seed: int, stream: int, base, amp, top=None) -> np.ndarray:
     return out
 
 
-def voxel_terrain(scene: Scene, seed: int, side: int, origin: int = 24):
-    """C5's voxel world (SURVEY.md §8d): a value-noise heightmap over side x side columns starting
-    at (origin, origin), heights in [48, 176); every column holds its top block plus the blocks a
-    lower neighbour exposes, all unit cubes [x, x+1)^3 (one octree cell each, DESIGN.md §4).
-    Faces W, E, Bottom, Top, South, North take materials of 16x16 block textures by block kind:
-    sand below 64, snow from 150, grass otherwise; exposed blocks below the top are dirt (3 deep)
-    then stone.  Returns (cuboids [n, 6], face materials [n, 6])."""
+def block_materials(scene: Scene, seed: int) -> dict:
+    """Register the BLOCK_TILES textures / materials; returns tile name -> material index."""
     if not scene.textures:
         scene.textures = [Texture()]
         scene.materials = [air_material(0)]
@@ -490,6 +500,17 @@ def voxel_terrain(scene: Scene, seed: int, side: int, origin: int = 24):
         scene.textures.append(Texture.image(block_tile(seed, 300 + k, base, amp, top)))
         scene.materials.append(Material(texture_index=len(scene.textures) - 1))
         mat[name] = len(scene.materials) - 1
+    return mat
+
+
+def voxel_terrain(scene: Scene, seed: int, side: int, origin: int = 24):
+    """C5's voxel world (SURVEY.md §8d): a value-noise heightmap over side x side columns starting
+    at (origin, origin), heights in [48, 176); every column holds its top block plus the blocks a
+    lower neighbour exposes, all unit cubes [x, x+1)^3 (one octree cell each, DESIGN.md §4).
+    Faces W, E, Bottom, Top, South, North take materials of 16x16 block textures by block kind:
+    sand below 64, snow from 150, grass otherwise; exposed blocks below the top are dirt (3 deep)
+    then stone.  Returns (cuboids [n, 6], face materials [n, 6])."""
+    mat = block_materials(scene, seed)
     # face order W, E, Bottom, Top, South, North (cuboid.rs:9-29)
     kinds = np.array([[mat["grass_side"]] * 2 + [mat["dirt"], mat["grass_top"]] + [mat["grass_side"]] * 2,
                       [mat["dirt"]] * 6, [mat["stone"]] * 6,
@@ -512,6 +533,142 @@ def voxel_terrain(scene: Scene, seed: int, side: int, origin: int = 24):
     z = zz.ravel()[col] + origin
     lo3 = np.stack([x, y, z], 1).astype(F32)
     return np.concatenate([lo3, lo3 + F32(1.0)], 1), kinds[kind]
+
+
+# ---------------------------------------------------------------------------- block models (C19)
+# Face order of the reference's block-model Cuboid (resource_manager.rs:583-588).
+MODEL_FACES = ("west", "east", "down", "up", "north", "south")
+
+
+def _rotation(axis: str, angle_deg: float) -> np.ndarray:
+    a = np.float32(np.deg2rad(angle_deg))
+    c, s = np.float32(np.cos(a)), np.float32(np.sin(a))
+    if axis == "x":
+        return np.array([[1, 0, 0], [0, c, -s], [0, s, c]], F32)
+    if axis == "y":
+        return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]], F32)
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]], F32)
+
+
+def element_quads(frm, to, faces: dict, rotation=None) -> list:
+    """One Minecraft block-model element (from / to in 1/16 block) -> voxel-local quad rows: the
+    per-face origin / u / v of Quad::from_face_name (quad.rs:26-68, the commented-out body), the
+    face uv rectangle / 16 as texture ranges, and an optional element rotation (origin in 1/16,
+    axis, degrees) applied as Quad::transform_about_pivot (quad.rs:115-125).
+    faces: name -> material or (material, (u1, v1, u2, v2))."""
+    f = np.asarray(frm, F32) / F32(16.0)
+    t = np.asarray(to, F32) / F32(16.0)
+    geo = {
+        "down": ((f[0], f[1], f[2]), (t[0] - f[0], 0, 0), (0, 0, t[2] - f[2])),
+        "up": ((t[0], t[1], f[2]), (f[0] - t[0], 0, 0), (0, 0, t[2] - f[2])),
+        "north": ((t[0], f[1], f[2]), (f[0] - t[0], 0, 0), (0, t[1] - f[1], 0)),
+        "south": ((f[0], f[1], t[2]), (t[0] - f[0], 0, 0), (0, t[1] - f[1], 0)),
+        "west": ((f[0], f[1], f[2]), (0, 0, t[2] - f[2]), (0, t[1] - f[1], 0)),
+        "east": ((t[0], f[1], t[2]), (0, 0, f[2] - t[2]), (0, t[1] - f[1], 0)),
+    }
+    rows = []
+    for name in MODEL_FACES:
+        if name not in faces:
+            continue
+        spec = faces[name]
+        mat, uv = (spec, (0.0, 0.0, 16.0, 16.0)) if np.isscalar(spec) else spec
+        o, u, v = (np.asarray(x, F32) for x in geo[name])
+        if rotation is not None:
+            piv = np.asarray(rotation[0], F32) / F32(16.0)
+            m = _rotation(rotation[1], rotation[2])
+            o = (m @ (o - piv)).astype(F32) + piv
+            u = (m @ u).astype(F32)
+            v = (m @ v).astype(F32)
+        uv = np.asarray(uv, F32) / F32(16.0)
+        rows.append((o, int(mat), u, v, (uv[0], uv[2]), (uv[1], uv[3]), (0, 0)))
+    return rows
+
+
+def alpha_tile(seed: int, stream: int, base, amp, mask: np.ndarray) -> np.ndarray:
+    """block_tile with alpha 0 where mask is False (plants, glass panes: transparent texels)."""
+    out = block_tile(seed, stream, base, amp)
+    out[..., 3] = np.where(mask, 255, 0).astype(np.uint8)
+    return out
+
+
+def block_models(scene: Scene, seed: int) -> dict:
+    """A small Minecraft-style block-model set: slab, stairs, cross plant, fence
+    post, tilted torch and glass pane.  Appends their textures, materials, quads and models to the
+    scene and returns name -> model index."""
+    def tile(name, img):
+        scene.textures.append(Texture.image(img))
+        scene.materials.append(Material(texture_index=len(scene.textures) - 1))
+        return len(scene.materials) - 1
+
+    planks = tile("planks", block_tile(seed, 350, (162, 130, 78), 20))
+    blades = scene_uniform(seed, 351, 256).reshape(16, 16) < 0.45
+    blades[:, ::3] = False
+    plant = tile("plant", alpha_tile(seed, 352, (70, 150, 40), 30, blades))
+    torch = tile("torch", block_tile(seed, 353, (120, 90, 40), 20, ((255, 210, 90), 3)))
+    frame = np.zeros((16, 16), bool)
+    frame[[0, 15], :] = frame[:, [0, 15]] = True
+    glass = tile("glass", alpha_tile(seed, 354, (200, 225, 235), 10, frame))
+    all6 = lambda m: {k: m for k in MODEL_FACES}  # noqa: E731
+    defs = {
+        "slab": [element_quads((0, 0, 0), (16, 8, 16), {**all6(planks), **{k: (planks, (0, 8, 16, 16)) for k in
+                                                                           ("west", "east", "north", "south")}})],
+        "stairs": [element_quads((0, 0, 0), (16, 8, 16), all6(planks)),
+                   element_quads((8, 8, 0), (16, 16, 16), all6(planks))],
+        "plant": [element_quads((0.8, 0, 8), (15.2, 16, 8), {"north": plant, "south": plant}, ((8, 8, 8), "y", 45.0)),
+                  element_quads((8, 0, 0.8), (8, 16, 15.2), {"west": plant, "east": plant}, ((8, 8, 8), "y", 45.0))],
+        "post": [element_quads((6, 0, 6), (10, 16, 10), all6(planks))],
+        "torch": [element_quads((7, 0, 7), (9, 10, 9), all6(torch), ((8, 0, 8), "x", -22.5))],
+        "pane": [element_quads((7, 0, 0), (9, 16, 16), all6(glass))],
+    }
+    rows, models, ids = [], [], {}
+    for name, elems in defs.items():
+        quads = [q for e in elems for q in e]
+        ids[name] = len(models)
+        models.append((len(rows), len(quads)))
+        rows.extend(quads)
+    base = len(scene.quads)
+    q = np.zeros(len(rows), _lib.QUAD_DTYPE)
+    for i, (o, m, u, v, tu, tv, _) in enumerate(rows):
+        q[i] = (o, m, u, v, tu, tv, (0, 0))
+    scene.quads = np.concatenate([scene.quads, q])
+    mb = len(scene.models)
+    scene.models = np.concatenate([np.asarray(scene.models, np.uint32).reshape(-1, 2),
+                                   np.array([(base + a, n) for a, n in models], np.uint32).reshape(-1, 2)])
+    return {k: mb + v for k, v in ids.items()}
+
+
+def place_models(scene: Scene, seed: int, ids: dict, positions: np.ndarray, stream: int = 360):
+    """Append block-model instances (unit-voxel cuboids with a cuboid_model entry) at integer
+    voxel positions [n, 3]; the model per position is drawn from `ids` with plants most likely."""
+    n = len(positions)
+    names = list(ids)
+    weights = np.array([0.10 if k != "plant" else 0.50 for k in names], np.float64)
+    cdf = np.cumsum(weights / weights.sum())
+    pick = np.searchsorted(cdf, scene_uniform(seed, stream, n).astype(np.float64), side="right")
+    model = np.array([ids[names[min(i, len(names) - 1)]] for i in pick], np.uint32)
+    lo = np.asarray(positions, F32)
+    box = np.concatenate([lo, lo + F32(1.0)], 1)
+    old = len(scene.cuboids)
+    cm = scene.cuboid_model if scene.cuboid_model is not None else np.full(old, _lib.MODEL_NONE, np.uint32)
+    scene.cuboids = np.concatenate([scene.cuboids.reshape(-1, 6), box]).astype(F32)
+    fm = np.zeros((n, 6), np.uint32)  # unused by model instances; any valid material
+    scene.cuboid_material = np.concatenate([scene.cuboid_material.reshape(-1, 6), fm]).astype(np.uint32)
+    scene.cuboid_model = np.concatenate([cm, model]).astype(np.uint32)
+
+
+def voxel_blocks(scene: Scene, seed: int, positions: np.ndarray):
+    """Grass blocks (voxel_terrain's textures) at integer positions [n, 3]: (cuboids, face materials)."""
+    m = block_materials(scene, seed)
+    face = np.array([m["grass_side"]] * 2 + [m["dirt"], m["grass_top"]] + [m["grass_side"]] * 2, np.uint32)
+    lo = np.asarray(positions, F32)
+    return np.concatenate([lo, lo + F32(1.0)], 1), np.tile(face, (len(lo), 1))
+
+
+def terrain_tops(seed: int, side: int, origin: int = 24) -> np.ndarray:
+    """The top block of every voxel_terrain column, [side * side, 3] integer (x, y, z)."""
+    hmap = (48 + np.floor(128 * _value_noise(seed, 400, side, side, [(6, 6), (12, 12), (24, 24), (48, 48)])))
+    zz, xx = np.meshgrid(np.arange(side), np.arange(side), indexing="ij")
+    return np.stack([xx.ravel() + origin, hmap.astype(np.int64).ravel(), zz.ravel() + origin], 1)
 
 
 def _assign_materials(ids, seed, n, stream=7):
@@ -539,7 +696,7 @@ def random_cuboids(seed: int, n: int, world: float, emin: float, emax: float):
     return np.concatenate([lo, np.minimum(lo + ext, F32(world - 0.001))], axis=1).astype(F32)
 
 
-CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny")
+CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny", "blocks")
 
 
 C5_SIDE = 1000  # columns per side: 1,001,225 unit blocks with the exposed-side fill
@@ -568,6 +725,18 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
         sc.cuboid_material = cm
         cam = Camera.look_at((16.0, 20.0, -14.0), (16.0, 16.0, 16.0))
         rs = RenderSettings(64, 48, 4, seed=seed)
+    elif name == "blocks":
+        # block-model test world: a 24 x 24 floor of grass blocks with every model
+        # of block_models() on it, close up
+        depth = 5
+        floor = np.stack(np.meshgrid(np.arange(4, 28), np.arange(4, 28), indexing="ij"), -1).reshape(-1, 2)
+        pos = np.stack([floor[:, 0], np.full(len(floor), 8), floor[:, 1]], 1)
+        sc.cuboids, sc.cuboid_material = voxel_blocks(sc, seed, pos)
+        ids_m = block_models(sc, seed)
+        on = pos[(pos[:, 0] + 2 * pos[:, 2]) % 3 == 0] + np.array([0, 1, 0])
+        place_models(sc, seed, ids_m, on)
+        cam = Camera.look_at((6.0, 16.0, -4.0), (16.0, 9.0, 16.0))
+        rs = RenderSettings(64, 48, 4, seed=seed)
     elif name == "C2":
         ids = primitive_materials(sc)
         depth = 6
@@ -595,6 +764,11 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
     elif name == "C5":
         depth = 11
         sc.cuboids, sc.cuboid_material = voxel_terrain(sc, seed, C5_SIDE)
+        # block models (§8f row 1, C19) on 3 % of the grass / sand surface columns
+        ids_m = block_models(sc, seed)
+        tops = terrain_tops(seed, C5_SIDE)
+        keep = (scene_uniform(seed, 361, len(tops)) < 0.03) & (tops[:, 1] < 150)
+        place_models(sc, seed, ids_m, tops[keep] + np.array([0, 1, 0]))
         mid = 24 + C5_SIDE / 2
         cam = Camera.look_at((mid, 230.0, 24.0 - 60.0), (mid, 100.0, mid))
         rs = RenderSettings(3840, 2160, 1024, seed=seed)

@@ -399,6 +399,8 @@ typedef struct {
     int inside;  /* origin inside the primitive: exit hit */
     int axis;    /* cuboid face axis */
     v3 n;        /* outward normal */
+    int64_t quad;        /* block-model hit: the global quad index, else -1 [C19] */
+    float alpha, beta;   /* its Quad::hit barycentrics */
 } prim_hit;
 
 /* Sphere::hit dead code after todo!() (geometry/sphere.rs:33-57) + [C2] root selection */
@@ -460,6 +462,73 @@ static int cuboid_test(const float *bx, const ray_t *r, int self_prim, prim_hit 
     return 1;
 }
 
+/* ---- block models [C19] ---- */
+#define MODEL_NONE 0xFFFFFFFFu
+#define QUAD_KEY 0x40000000u /* last_prim of a ray leaving quad q: QUAD_KEY | q */
+typedef struct { v3 o, u, v, w, n; float d; } quad_geo;
+
+/* Quad::new (geometry/quad.rs:90-114): n = u x v, normal = normalize(n), w = n / n.n, d = normal.origin */
+static quad_geo quad_geometry(const ref_quad *q) {
+    quad_geo g;
+    g.o = V(q->origin[0], q->origin[1], q->origin[2]);
+    g.u = V(q->u[0], q->u[1], q->u[2]);
+    g.v = V(q->v[0], q->v[1], q->v[2]);
+    v3 n = vcross(g.u, g.v);
+    g.n = vnorm(n);
+    float nn = vdot(n, n);
+    g.w = V(n.x / nn, n.y / nn, n.z / nn);
+    g.d = vdot(g.n, g.o);
+    return g;
+}
+
+/* Quad::hit (geometry/quad.rs:172-200): voxel-local, back faces culled, 0 < t <= t_next */
+static int quad_hit(const quad_geo *g, const ray_t *r, v3 voxel, float t_next, float *t_out, float *alpha,
+                    float *beta) {
+    v3 tro = vsub(r->o, voxel);
+    float denom = vdot(r->d, g->n);
+    if (denom >= -RAY_EPSILON) return 0;
+    float t = (g->d - vdot(g->n, tro)) / denom;
+    if (t <= 0.0f || t > t_next) return 0;
+    v3 inter = vadd(tro, vscale(r->d, t));
+    v3 planar = vsub(inter, g->o);
+    float a = vdot(g->w, vcross(planar, g->v));
+    float b = vdot(g->w, vcross(g->u, planar));
+    if (!(a >= 0.0f && a <= 1.0f) || !(b >= 0.0f && b <= 1.0f)) return 0;
+    *t_out = t;
+    *alpha = a;
+    *beta = b;
+    return 1;
+}
+
+/* a block-model leaf (ResourceModel::Quad, octree_traversal.rs:207-213) [C19]: the closest of the
+ * model's quads with 0 < t <= t_accept, ties to the later quad (`t > t_next` rejects), skipping
+ * the quad the ray leaves */
+static int model_test(const ref_scene *s, const ray_t *r, uint32_t ci, uint32_t mdl, float t_accept, prim_hit *h) {
+    const float *bx = &s->cuboids[6 * (size_t)ci];
+    v3 voxel = V(bx[0], bx[1], bx[2]);
+    uint32_t first = s->model_quads[2 * (size_t)mdl], cnt = s->model_quads[2 * (size_t)mdl + 1];
+    float t_next = t_accept;
+    int found = 0;
+    for (uint32_t k = 0; k < cnt; k++) {
+        uint32_t q = first + k;
+        if ((QUAD_KEY | q) == r->last_prim) continue;
+        quad_geo g = quad_geometry(&s->quads[q]);
+        float t, a, b;
+        if (quad_hit(&g, r, voxel, t_next, &t, &a, &b)) {
+            t_next = t;
+            h->quad = q;
+            h->alpha = a;
+            h->beta = b;
+            h->n = g.n;
+            found = 1;
+        }
+    }
+    h->t = t_next;
+    h->inside = 0;
+    h->axis = 0;
+    return found;
+}
+
 /* Face enum index from outward normal (geometry/cuboid.rs:9-29) */
 static inline int face_index(int axis, float sgn) {
     if (axis == 0) return sgn < 0.0f ? 0 : 1; /* West(-X), East(+X) */
@@ -474,7 +543,14 @@ static void commit_hit(ctx_t *c, ray_t *r, uint32_t prim, const prim_hit *h) {
     float u, v;
     uint32_t mat;
     v3 n;
-    if (!(prim & PRIM_CUBOID_BIT)) {
+    if (h->quad >= 0) { /* block-model quad [C19]: uv from the barycentrics (quad.rs:194-197) */
+        const ref_quad *q = &s->quads[h->quad];
+        n = h->n;
+        u = q->texture_u_range[0] + h->alpha * (q->texture_u_range[1] - q->texture_u_range[0]);
+        v = q->texture_v_range[0] + h->beta * (q->texture_v_range[1] - q->texture_v_range[0]);
+        mat = q->material;
+        prim = QUAD_KEY | (uint32_t)h->quad;
+    } else if (!(prim & PRIM_CUBOID_BIT)) {
         const float *sp = &s->spheres[4 * (size_t)prim];
         v3 cen = V(sp[0], sp[1], sp[2]);
         float rad = sp[3];
@@ -534,7 +610,10 @@ static int leaf_test(ctx_t *c, const ray_t *r, uint32_t leaf, float t_exit_w, fl
         int self_prim = (prim == r->last_prim);
         int ok;
         c->st.prim_tests++;
+        h.quad = -1;
+        uint32_t mdl = (prim & PRIM_CUBOID_BIT) && s->cuboid_model ? s->cuboid_model[prim & ~PRIM_CUBOID_BIT] : MODEL_NONE;
         if (!(prim & PRIM_CUBOID_BIT)) ok = sphere_test(&s->spheres[4 * (size_t)prim], r, self_prim, &h);
+        else if (mdl != MODEL_NONE) ok = model_test(s, r, prim & ~PRIM_CUBOID_BIT, mdl, t_accept, &h);
         else ok = cuboid_test(&s->cuboids[6 * (size_t)(prim & ~PRIM_CUBOID_BIT)], r, self_prim, &h);
         if (ok && h.t <= t_accept && (!found || h.t < best->t)) {
             *best = h;
@@ -1404,6 +1483,19 @@ void ref_intersect_brute(const ref_scene *s, const float *rays, uint32_t n, floa
         }
         out_t[i] = best;
         out_prim[i] = bp;
+    }
+}
+
+void ref_quad_hit(const ref_quad *q, const float *rays, const float voxel[3], uint32_t n, float *out, uint8_t *hit) {
+    quad_geo g = quad_geometry(q);
+    for (uint32_t i = 0; i < n; i++) {
+        ray_t r;
+        ray_new(&r, V(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]), V(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
+        float t = 0.0f, a = 0.0f, b = 0.0f;
+        hit[i] = (uint8_t)quad_hit(&g, &r, V(voxel[0], voxel[1], voxel[2]), INFINITY, &t, &a, &b);
+        out[3 * i] = t;
+        out[3 * i + 1] = a;
+        out[3 * i + 2] = b;
     }
 }
 

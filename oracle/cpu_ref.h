@@ -49,6 +49,18 @@ typedef struct {
     uint64_t offset; /* byte offset into the texel pool */
 } ref_texture;
 
+/* Block-model quad: geometry::quad::Quad::new arguments (src/geometry/quad.rs:90-114) in
+ * voxel-local units; the same 64-byte layout as octpt_quad (include/octpt.h). */
+typedef struct {
+    float origin[3];
+    uint32_t material;
+    float u[3];
+    float v[3];
+    float texture_u_range[2];
+    float texture_v_range[2];
+    uint32_t reserved[2];
+} ref_quad;
+
 /* Sun + sampling strategy, reference src/scene/mod.rs:60-127, 271-383. */
 typedef struct {
     float azimuth, altitude, radius;
@@ -87,6 +99,13 @@ typedef struct {
     ref_sun sun;
     int32_t emitters_enabled;
     float f_sub_surface; /* Scene::f_sub_surface (scene/mod.rs:152), path_tracer.rs:237-241 */
+    /* block models: cuboid_model NULL or one entry per cuboid (0xFFFFFFFF = plain
+     * box); model m owns quads[model_quads[2m] .. + model_quads[2m+1]) */
+    const uint32_t *cuboid_model;
+    const uint32_t *model_quads;
+    uint32_t n_models;
+    const ref_quad *quads;
+    uint32_t n_quads;
 } ref_scene;
 
 typedef struct {
@@ -144,6 +163,9 @@ void ref_intersect(const ref_scene *s, const float *rays, const uint32_t *last_p
                    uint32_t n, float *out_t, uint32_t *out_prim, float *out_normal, uint32_t *out_steps);
 /* brute force over all primitives (no octree), same primitive semantics */
 void ref_intersect_brute(const ref_scene *s, const float *rays, uint32_t n, float *out_t, uint32_t *out_prim);
+/* Quad::hit (quad.rs:172-200) of one quad for n rays (n*6 floats) at voxel position `voxel`, with
+ * t_next = +inf: out n*3 floats (t, alpha, beta), hit flags n bytes.  KAT hook for tests. */
+void ref_quad_hit(const ref_quad *q, const float *rays, const float voxel[3], uint32_t n, float *out, uint8_t *hit);
 
 /* --- render: progressive running mean (TileRenderer::render_tile_average) ---
  * accum: W*H*4 floats, in/out (initialise to F32Color::BLACK = 0,0,0,1).

@@ -53,7 +53,8 @@ class RefScene(C.Structure):
                 ("cuboid_material", C.c_void_p), ("n_cuboids", C.c_uint32), ("materials", C.c_void_p),
                 ("n_materials", C.c_uint32), ("textures", C.c_void_p), ("n_textures", C.c_uint32),
                 ("texels", C.c_void_p), ("sun", RefSun), ("emitters_enabled", C.c_int32),
-                ("f_sub_surface", C.c_float)]
+                ("f_sub_surface", C.c_float), ("cuboid_model", C.c_void_p), ("model_quads", C.c_void_p),
+                ("n_models", C.c_uint32), ("quads", C.c_void_p), ("n_quads", C.c_uint32)]
 
 
 class RefParams(C.Structure):
@@ -115,6 +116,8 @@ def load() -> C.CDLL:
     lib.ref_intersect.argtypes = [C.POINTER(RefScene), vp, vp, vp, u32, vp, vp, vp, vp]
     lib.ref_intersect_brute.restype = None
     lib.ref_intersect_brute.argtypes = [C.POINTER(RefScene), vp, u32, vp, vp]
+    lib.ref_quad_hit.restype = None
+    lib.ref_quad_hit.argtypes = [vp, vp, vp, u32, vp, vp]
     lib.ref_render.restype = C.c_int
     lib.ref_render.argtypes = [C.POINTER(RefScene), C.POINTER(RefCamera), C.POINTER(RefParams), vp, vp,
                                C.POINTER(RefStats)]
@@ -205,6 +208,15 @@ class OracleScene:
                           len(sp), _p(cb), _p(cm), len(cb), C.cast(mats, C.c_void_p), len(scene.materials),
                           C.cast(texs, C.c_void_p), len(scene.textures), _p(texels), sun, int(scene.emitters_enabled),
                           scene.f_sub_surface)
+        if scene.cuboid_model is not None and len(scene.cuboids):
+            self.s.cuboid_model = _p(k(scene.cuboid_model, np.uint32))
+            mq = k(np.asarray(scene.models, np.uint32).reshape(-1, 2), np.uint32)
+            self.s.model_quads = _p(mq)
+            self.s.n_models = len(mq)
+            qd = np.ascontiguousarray(scene.quads)
+            self._keep.append(qd)
+            self.s.quads = qd.ctypes.data
+            self.s.n_quads = len(qd)
 
 
 def render(scene, camera, width, height, spp, *, spp_start=0, max_depth=5, seed=1, threads=8, forward=False,
@@ -267,6 +279,20 @@ def intersect_brute(scene, rays):
     prim = np.zeros(n, np.uint32)
     lib.ref_intersect_brute(C.byref(os_.s), _p(rays), n, _p(t), _p(prim))
     return t, prim
+
+
+def quad_hit(quad_row, rays, voxel):
+    """Quad::hit of one octpt_quad row (numpy QUAD_DTYPE record) for rays [n, 6] at `voxel`:
+    (t, alpha, beta) [n, 3] and hit flags [n]."""
+    lib = load()
+    q = np.ascontiguousarray(np.asarray([quad_row]))
+    r = np.ascontiguousarray(rays, np.float32)
+    v = np.ascontiguousarray(voxel, np.float32)
+    n = len(r)
+    out = np.zeros((n, 3), np.float32)
+    hit = np.zeros(n, np.uint8)
+    lib.ref_quad_hit(q.ctypes.data, _p(r), _p(v), n, _p(out), _p(hit))
+    return out, hit.astype(bool)
 
 
 def tonemap(accum):

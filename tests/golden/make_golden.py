@@ -31,7 +31,8 @@ RENDERS = {
     "c2_small": ("C2", 160, 90, 4, None),
     "c3_small": ("C3", 96, 54, 2, None),
     "c4_small": ("C4", 64, 36, 2, None),  # cuboids + image textures (procedural, scene.py)
-    "c5_small": ("C5", 96, 54, 2, None),  # 1 M unit-block voxel terrain, depth 11
+    "c5_small": ("C5", 96, 54, 2, None),  # 1 M unit-block voxel terrain + block models, depth 11
+    "blocks_small": ("blocks", 64, 48, 4, None),  # block-model quads
     # sun sampling (next-event estimation): config + scene.SUN_VARIANTS entry
     "tiny_fast": ("tiny", 64, 48, 4, None, "fast"),
     "c2_hq": ("C2", 160, 90, 2, None, "hq"),
@@ -43,6 +44,7 @@ PREVIEWS = {
     "c3_preview": ("C3", 192, 108),
     "c4_preview": ("C4", 128, 72),  # transparent texels exercise the pass-through loop
     "c5_preview": ("C5", 160, 90),
+    "blocks_preview": ("blocks", 128, 96),
 }
 
 

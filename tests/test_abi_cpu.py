@@ -18,7 +18,8 @@ HEADER = ROOT / "include" / "octpt.h"
 STRUCTS = {"octpt_octant": "Octant", "octpt_sphere": "Sphere", "octpt_cuboid": "Cuboid",
            "octpt_material": "Material", "octpt_texture": "Texture", "octpt_sun": "Sun",
            "octpt_scene_desc": "SceneDesc", "octpt_camera": "Camera", "octpt_render_params": "RenderParams",
-           "octpt_stats": "Stats", "octpt_octree_view": "OctreeView"}
+           "octpt_stats": "Stats", "octpt_octree_view": "OctreeView", "octpt_quad": "Quad",
+           "octpt_block_model": "BlockModel"}
 
 
 def header_functions():

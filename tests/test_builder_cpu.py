@@ -21,7 +21,7 @@ def _same(sc):
     return t
 
 
-@pytest.mark.parametrize("name", ["C1", "tiny", "C2", "C3", "C5"])
+@pytest.mark.parametrize("name", ["C1", "tiny", "C2", "C3", "C5", "blocks"])
 def test_builder_configs(name):
     sc, _, _ = S.make_config(name)
     t = _same(sc)

@@ -12,7 +12,7 @@ from octree_pathtracing_amd import scene as S
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
 RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c5_small", "c3_preview", "c4_preview",
-           "c5_preview", "tiny_fast", "c2_hq", "c4_hq_sss", "c5_nee_importance"]
+           "c5_preview", "tiny_fast", "c2_hq", "c4_hq_sss", "c5_nee_importance", "blocks_small", "blocks_preview"]
 STAT_KEYS = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
              "texel_reads", "max_path_segs")
 

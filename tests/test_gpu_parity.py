@@ -89,7 +89,8 @@ def assert_parity(gpu, ref, tag):
 
 
 @pytest.mark.parametrize("name,res", [("tiny", None), ("C1", None), ("C1-as-is", None), ("C2", (160, 90, 8)),
-                                      ("C3", (192, 108, 2)), ("C4", (128, 72, 2)), ("C5", (192, 108, 2))])
+                                      ("C3", (192, 108, 2)), ("C4", (128, 72, 2)), ("C5", (192, 108, 2)),
+                                      ("blocks", None)])
 def test_render_parity(torch_cuda, renderer, name, res):
     from octree_pathtracing_amd import scene as S
 
@@ -153,7 +154,7 @@ def test_intersect_parity(renderer):
     from octree_pathtracing_amd import scene as S
     from oracle import cpu_ref
 
-    for name in ("tiny", "C3"):
+    for name in ("tiny", "C3", "blocks"):
         sc, cam, rs = S.make_config(name)
         renderer.set_scene(sc)
         rng = np.random.default_rng(7)
@@ -229,6 +230,18 @@ def test_validation_errors(renderer):
     with pytest.raises(_lib.OctptError) as e:
         renderer.set_scene(bad)
     assert e.value.status == _lib.ERR_INVALID_ARG
+    for fault in ("stretched", "model_index"):  # block-model instances (C19)
+        blk = S.make_config("blocks")[0]
+        mi = int(np.nonzero(blk.cuboid_model != _lib.MODEL_NONE)[0][0])
+        if fault == "stretched":
+            blk.cuboids = blk.cuboids.copy()
+            blk.cuboids[mi, 4] += 0.5  # a model instance must be a unit voxel
+        else:
+            blk.cuboid_model = blk.cuboid_model.copy()
+            blk.cuboid_model[mi] = len(blk.models)
+        with pytest.raises(_lib.OctptError) as e:
+            renderer.set_scene(blk)
+        assert e.value.status == _lib.ERR_INVALID_ARG, fault
     renderer.set_scene(sc)
     p = renderer.params(rs.width, rs.height, 0, 1)
     p.branch_count = 10
@@ -312,7 +325,7 @@ def test_c3_grazing_self_hit_regression(torch_cuda, renderer):
     assert rel_err(acc[r0:r1], racc[r0:r1]).max() <= REL_TOL_FORWARD
 
 
-@pytest.mark.parametrize("name,res", [("tiny", None), ("C3", (256, 144, 4))])
+@pytest.mark.parametrize("name,res", [("tiny", None), ("C3", (256, 144, 4)), ("blocks", None)])
 def test_megakernel_equals_wavefront(torch_cuda, renderer, name, res):
     """Both GPU strategies compute every path with the same device functions: bit-identical."""
     from octree_pathtracing_amd import scene as S
@@ -353,7 +366,7 @@ GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
 
 @pytest.mark.parametrize("name", ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c5_small",
                                   "c3_preview", "c4_preview", "c5_preview", "tiny_fast", "c2_hq", "c4_hq_sss",
-                                  "c5_nee_importance"])
+                                  "c5_nee_importance", "blocks_small", "blocks_preview"])
 def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     """GPU render vs the committed oracle fixture (tests/golden/make_golden.py): exact per-pixel
     segment counts and work totals, radiance within REL_TOL_FORWARD."""
@@ -419,7 +432,7 @@ def test_split_extend_equals_default(torch_cuda, renderer, name, res):
 
 # ---------------------------------------------------------------------------- preview mode (C16)
 @pytest.mark.parametrize("name,res", [("tiny", None), ("C1", None), ("C2", (160, 90)), ("C3", (256, 144)),
-                                      ("C4", (160, 90)), ("C5", (320, 180))])
+                                      ("C4", (160, 90)), ("C5", (320, 180)), ("blocks", (160, 120))])
 def test_preview_parity(torch_cuda, renderer, name, res):
     """RendererMode::Preview (preview_kernel) vs the oracle: segment counts, work totals and the
     flat-shaded radiance bit-exact; alpha of the incoming buffer untouched."""
@@ -490,7 +503,8 @@ def test_renderer_preview_mode(renderer):
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("name,variant,res", [("tiny", "fast", None), ("tiny", "hq_sss", None),
                                               ("C2", "hq", (160, 90, 4)), ("C3", "fast", (192, 108, 2)),
-                                              ("C4", "hq_sss", (128, 72, 2)), ("C5", "nee_importance", (192, 108, 2))])
+                                              ("C4", "hq_sss", (128, 72, 2)), ("C5", "nee_importance", (192, 108, 2)),
+                                              ("blocks", "hq", None)])
 def test_sun_sampling_parity(torch_cuda, renderer, name, variant, res):
     from octree_pathtracing_amd import scene as S
 
