@@ -28,7 +28,7 @@ constexpr uint32_t kCounterRing = 256;
 constexpr uint64_t kMaxChunkPaths = 1ull << 30;    // colour buffer: up to 16 GiB of float4 per chunk
                                                     // (C3 = 530 M paths = one chunk: one drain tail)
 constexpr uint32_t kLookahead = 3;                  // host steering: iterations queued ahead of the check
-constexpr uint32_t kDefaultPool = 4u << 20;          // path slots in flight
+constexpr uint32_t kDefaultPool = 256u << 20;        // path slots in flight (28.7 GB of queues + path state)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
 constexpr uint32_t kDefaultRefill = 16;              // extend: idle lanes before a wave refills
 constexpr uint32_t kDefaultLeafBatch = 0;            // extend: parked lanes before a wave tests leaves (0: inline)
@@ -83,10 +83,11 @@ struct octpt_ctx {
     float build_ms = 0.0f;  // device time of the last octpt_build_octree_device
     BuildScratch build_scratch;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
-    int extend_bpc_cache[kMaxDepth + 1][3][3] = {};  // [depth][kPrims][variant]
+    int extend_bpc_cache[kMaxDepth + 1][3][4] = {};  // [depth][kPrims][variant]
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
-    size_t pool = 0, color_cap = 0;
+    size_t pool = 0, color_cap = 0, nee_pool = 0;  // nee_pool: slots of the sun-sampling planes (wb.pd)
+    void *nee_alloc = nullptr;
     std::vector<void *> wave_allocs;
     void *color_alloc = nullptr;
     uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
@@ -390,7 +391,9 @@ void free_wave(octpt_ctx *ctx) {
     ctx->wave_allocs.clear();
     if (ctx->color_alloc) (void)hipFree(ctx->color_alloc);
     ctx->color_alloc = nullptr;
-    ctx->pool = ctx->color_cap = 0;
+    if (ctx->nee_alloc) (void)hipFree(ctx->nee_alloc);
+    ctx->nee_alloc = nullptr;
+    ctx->pool = ctx->color_cap = ctx->nee_pool = 0;
     ctx->wb = WaveBuffers{};
 }
 
@@ -410,7 +413,7 @@ constexpr uint32_t kCountSpan = (kSegs - 1u) * kCtrStride + 1u;
 // queue segment capacity: seed wave w fills segment w % kSegs, so ceil(ceil(pool / 64) / kSegs) waves
 size_t seg_cap_for(size_t pool) { return ((pool + 63) / 64 + kSegs - 1) / kSegs * 64; }
 
-octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
+octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool nee) {
     if (!ctx->h_count) {
         HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), (kLookahead + 1) * kCountSpan * sizeof(uint32_t),
                                    hipHostMallocDefault));
@@ -431,7 +434,6 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pa));
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pb));
         HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pc));
-        HIP_TRY(ctx, wave_alloc(ctx, 4 * pool, &B.pd));
         B.pool = (uint32_t)pool;
         HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.hit));
         HIP_TRY(ctx, wave_alloc(ctx, kCtrlWords, &B.ctrl));
@@ -446,6 +448,17 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items) {
         ctx->color_cap = color_items;
     }
     ctx->wb.color = static_cast<float4 *>(ctx->color_alloc);
+    // sun-sampling planes (4 x 16 B per slot) only for scenes that sample the sun (C18)
+    if (nee && ctx->nee_pool < ctx->pool) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (ctx->nee_alloc) (void)hipFree(ctx->nee_alloc);
+        ctx->nee_alloc = nullptr;
+        ctx->nee_pool = 0;
+        HIP_TRY(ctx, hipMalloc(&ctx->nee_alloc, 4 * ctx->pool * sizeof(float4)));
+        ctx->nee_pool = ctx->pool;
+    }
+    ctx->wb.pd = static_cast<float4 *>(ctx->nee_alloc);
+    ctx->wb.pool = (uint32_t)ctx->pool;
     return OCTPT_OK;
 }
 
@@ -491,9 +504,9 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const uint32_t chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, ctx->chunk_cap / n_px));
     const uint64_t chunk_max = (uint64_t)chunk_spp * n_px;
     const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
-    octpt_status st = ensure_wave(ctx, pool, chunk_max);
+    octpt_status st = ensure_wave(ctx, pool, chunk_max, ctx->S.sun.sun_sampling != 0);
     if (st != OCTPT_OK) return st;
-    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)][ctx->leaf_batch == kLeafSplit ? 2 : (ctx->leaf_batch ? 1 : 0)];
+    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)][(ctx->leaf_batch & kLeafSpec) ? 3 : ctx->leaf_batch == kLeafSplit ? 2 : (ctx->leaf_batch ? 1 : 0)];
     if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S, ctx->leaf_batch);
     const int grid_extend = ctx->num_cu * bpc;
     if (std::getenv("OCTPT_DEBUG"))
@@ -704,6 +717,9 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->leaf_batch = std::min<uint32_t>(env_u32("OCTPT_LEAF_BATCH", kDefaultLeafBatch), 64u);
     if (const char *m = std::getenv("OCTPT_EXTEND")) {  // extend variant: "split" = wave-specialised
         if (std::string(m) == "split") ctx->leaf_batch = kLeafSplit;
+        if (std::string(m) == "spec")
+            ctx->leaf_batch = kLeafSpec | std::min<uint32_t>(env_u32("OCTPT_SPEC_BATCH", 16), 64u) |
+                              (std::min<uint32_t>(env_u32("OCTPT_SPEC_STALL", 8), 64u) << 8);
     }
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);

@@ -170,6 +170,8 @@ constexpr uint32_t kStatWords = kSegs * kStatRow;
 // extend variants (launch_wf_extend's leaf_batch): 0 leaf tests inline, 1..64 wave-local deferral,
 // kLeafSplit the wave-specialised kernel (3 traversal waves + 1 leaf-test wave per block)
 constexpr uint32_t kLeafSplit = 0xFFFFu;
+// speculative extend (wf_extend_spec_kernel): kLeafSpec | batch | stall << 8
+constexpr uint32_t kLeafSpec = 0x10000u;
 
 // kernel launchers (octpt_kernels.hip)
 hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,

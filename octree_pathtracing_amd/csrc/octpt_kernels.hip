@@ -261,28 +261,33 @@ __device__ __forceinline__ uint2 hit_record(uint32_t prim, const PrimHit &h) {
     return make_uint2((prim & kPrimCuboidBit) | ((h.f & 15u) << 27) | (prim & kPrimIndexMask), __float_as_uint(h.t));
 }
 
-// Sphere::hit restated (sphere.rs:33-57) + root selection [C2].  Straight-line: the near root is
-// computed for every lane (the common case), the far root only for lanes that need it (origin
-// inside the sphere, or re-entering the primitive the ray left).
+// Sphere::hit restated (sphere.rs:33-57) + root selection [C2].  The square root and divisions
+// run only for lanes that can still hit: 48 % of C3's sphere tests have disc < 0 and 28 % are
+// self tests, mostly of rays leaving outward, so the wave usually skips that block.
 __device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool self_prim, PrimHit &h) {
     const v3 oc = vsub(V(sp.x, sp.y, sp.z), r.o);
     const float a = vdot(r.d, r.d);
     const float hh = vdot(r.d, oc);
     const float cc = vdot(oc, oc) - sp.w * sp.w;
     const float disc = hh * hh - a * cc;
-    const bool real = disc >= 0.0f;
-    const float sq = sqrtf(disc);  // NaN when disc < 0: unused then
-    const float t0 = (hh - sq) / a;
-    const bool near_ok = real && !self_prim && t0 > RAY_EPSILON;
-    float t1 = 0.0f;
-    bool far_ok = false;
-    if (real && !near_ok && (!self_prim || r.self_inward)) {
-        t1 = (hh + sq) / a;
-        far_ok = t1 > RAY_EPSILON;
+    bool ok = false;
+    if (disc >= 0.0f && (!self_prim || r.self_inward)) {
+        const float sq = sqrtf(disc);
+        bool near_ok = false;
+        if (!self_prim) {
+            const float t0 = (hh - sq) / a;
+            near_ok = t0 > RAY_EPSILON;
+            h.t = t0;
+            h.f = 0u;
+        }
+        if (!near_ok) {
+            const float t1 = (hh + sq) / a;
+            h.t = t1;
+            h.f = 1u;
+        }
+        ok = near_ok || h.t > RAY_EPSILON;
     }
-    h.t = near_ok ? t0 : t1;
-    h.f = near_ok ? 0u : 1u;
-    return near_ok || far_ok;
+    return ok;
 }
 
 __device__ __forceinline__ float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6f : 1.0f / d; }
@@ -1189,6 +1194,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
 // material 0 or Sun::flat_shading (scene/mod.rs:447-452).  Coherent primary rays: one thread per
 // pixel in 8x8 tiles (one tile per wave), no queues.
 // ===========================================================================
+template <int kPrims>
 __global__ __launch_bounds__(kBlock) void preview_kernel(DevScene S, DevCamera C, DevRender R,
                                                          float4 *__restrict__ accum, uint32_t *__restrict__ segcount,
                                                          unsigned long long *__restrict__ stats) {
@@ -1232,7 +1238,7 @@ __global__ __launch_bounds__(kBlock) void preview_kernel(DevScene S, DevCamera C
             float ta;
             int rs;
             do {
-                rs = esvo_step<false>(S, tr, E, stk, cnt, prim, h, lf, ta);
+                rs = esvo_step<false, kPrims>(S, tr, E, stk, cnt, prim, h, lf, ta);
             } while (rs == kStepContinue);
             cnt.steps += E.iter;
             if (rs != kStepHit) break;  // a miss leaves the last hit record in place
@@ -1487,6 +1493,134 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
         }
     }
     cnt.segs = (threadIdx.x & 63u) == 0u ? segs_w : 0u;  // flush_counters sums over the wave's lanes
+    flush_counters(cnt, stats);
+}
+
+// ---------------------------------------------------------------------------
+// Speculative extend (OCTPT_EXTEND=spec): a lane reaching a leaf posts the leaf test as its pending
+// job and keeps traversing as if the leaf missed (the leaf-miss advance of esvo_step's resume
+// path).  The wave runs its pending leaf tests together, once `batch` lanes hold one, `stall`
+// lanes are stalled, or no lane can step.  A hit of the job is the ray's answer (leaves are
+// visited front to back, so the speculative steps taken since are discarded, and so are their
+// counts); a miss means the speculation was the traversal.  A lane reaching a second leaf, or
+// the end of its ray, while its job is pending waits for the batch.  Results and counters equal
+// wf_extend_kernel's exactly.
+// ---------------------------------------------------------------------------
+template <int kPrims>
+__global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_spec_kernel(DevScene S, WaveBuffers B, uint32_t q,
+                                                                                uint32_t refill, uint32_t spec,
+                                                                                unsigned long long *__restrict__ stats) {
+    extern __shared__ uint2 lds_stack[];
+    const Stack stk = stack_of(lds_stack, S.depth);
+    const uint32_t batch = spec & 0xFFu, stall_max = (spec >> 8) & 0xFFu;
+    const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
+    if (blockIdx.x == 0 && threadIdx.x < kSegs) {
+        B.ctrl[ctr_count(q ^ 1u, threadIdx.x)] = 0u;
+        B.ctrl[ctr_head(q ^ 1u, threadIdx.x)] = 0u;
+    }
+    uint32_t seg = __builtin_amdgcn_readfirstlane(((blockIdx.x * kBlock + threadIdx.x) >> 6) % kSegs);
+    uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
+    bool rays_left = true;
+    uint32_t segs_w = 0u;
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    bool active = false;  // the lane owns a ray
+    bool job = false;     // a leaf test is pending: (jleaf, jt, jiter)
+    bool wait = false;    // stalled until the batch: a second leaf (E.resume set) or the ray's end (fin)
+    bool fin = false;
+    uint32_t pos = 0u, jiter = 0u;
+    uint2 jleaf = make_uint2(0u, 0u);
+    float jt = 0.0f;
+    TraceRay tr;
+    Esvo E;
+    uint2 leaf = make_uint2(0u, 0u);
+    float t_accept = 0.0f;
+    for (;;) {
+        const bool idle = !active;
+        const uint64_t im = __ballot(idle);
+        if (rays_left && im != 0ull && ((uint32_t)__popcll(im) >= refill || ~im == 0ull)) {
+            const uint32_t my = wave_ticket(B.ctrl + ctr_head(q, seg), idle);
+            bool dry = false;
+            if (idle) {
+                if (my < seg_n) {
+                    pos = seg * B.seg_cap + my;
+                    const float4 r0 = ray0[pos], r1 = ray1[pos];
+                    tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
+                                        (__float_as_uint(r1.w) >> 31) != 0u);
+                    esvo_begin(S, tr, E, stk);
+                    active = true;
+                } else {
+                    dry = true;
+                }
+            }
+            segs_w += (uint32_t)__popcll(__ballot(idle && !dry));
+            if (__ballot(dry) != 0ull) {
+                const uint32_t j = threadIdx.x & 63u;
+                const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, j)) < B.ctrl[ctr_count(q, j)]);
+                rays_left = m != 0ull;
+                if (rays_left) {
+                    seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
+                    seg_n = B.ctrl[ctr_count(q, seg)];
+                }
+            }
+        }
+        const uint64_t am = __ballot(active);
+        if (am == 0ull && !rays_left) break;
+        const uint64_t jm = __ballot(job);
+        const uint64_t sm = __ballot(active && !wait);
+        if (jm != 0ull &&
+            ((uint32_t)__popcll(jm) >= batch || (uint32_t)__popcll(__ballot(wait)) >= stall_max || sm == 0ull)) {
+            if (job) {
+                job = false;
+                uint32_t prim = kPrimNone;
+                PrimHit h;
+                if (leaf_test<kPrims>(S, tr, jleaf, jt, prim, h, cnt)) {
+                    B.hit[pos] = hit_record(prim, h);
+                    cnt.steps += jiter;
+                    active = false;
+                    wait = false;
+                    fin = false;
+                } else if (wait) {
+                    wait = false;
+                    if (fin) {  // the speculation ran to the ray's end: a miss
+                        fin = false;
+                        B.hit[pos] = make_uint2(kPrimNone, 0u);
+                        cnt.steps += E.iter;
+                        active = false;
+                    } else {  // the stalled second leaf becomes the job; E.resume advances past it
+                        job = true;
+                        jleaf = leaf;
+                        jt = t_accept;
+                        jiter = E.iter;
+                    }
+                }
+            }
+        }
+        if (active && !wait) {
+            uint32_t prim = kPrimNone;
+            PrimHit h;
+            const int rs = esvo_step<true, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
+            if (rs == kStepLeaf) {
+                if (!job) {
+                    job = true;
+                    jleaf = leaf;
+                    jt = t_accept;
+                    jiter = E.iter;
+                } else {
+                    wait = true;
+                }
+            } else if (rs != kStepContinue) {  // kStepMiss (leaves are tested in the batch)
+                if (job) {
+                    wait = true;
+                    fin = true;
+                } else {
+                    B.hit[pos] = make_uint2(kPrimNone, 0u);
+                    cnt.steps += E.iter;
+                    active = false;
+                }
+            }
+        }
+    }
+    cnt.segs = (threadIdx.x & 63u) == 0u ? segs_w : 0u;
     flush_counters(cnt, stats);
 }
 
@@ -1818,6 +1952,10 @@ int render_blocks_per_cu(uint32_t depth) {
 // the extend instance a scene / setting launches (sphere-only scenes: no slab test).
 // leaf_batch: 0 inline leaf tests, 1..64 wave-local deferral, kLeafSplit the wave-specialised kernel
 static const void *extend_instance(const DevScene &S, uint32_t leaf_batch) {
+    if (leaf_batch & kLeafSpec)
+        return S.has_models ? reinterpret_cast<const void *>(wf_extend_spec_kernel<kPrimsModels>)
+               : S.has_cuboids ? reinterpret_cast<const void *>(wf_extend_spec_kernel<kPrimsBoxes>)
+                               : reinterpret_cast<const void *>(wf_extend_spec_kernel<kPrimsSpheres>);
     if (leaf_batch == kLeafSplit)
         return S.has_cuboids ? reinterpret_cast<const void *>(wf_extend_split_kernel<kPrimsModels>)
                              : reinterpret_cast<const void *>(wf_extend_split_kernel<kPrimsSpheres>);
@@ -1847,8 +1985,14 @@ int extend_blocks_per_cu(const DevScene &S, uint32_t leaf_batch) {
 hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
                           uint32_t *segcount, unsigned long long *stats, hipStream_t stream) {
     const uint32_t grid = (R.total_items + kBlock - 1u) / kBlock;
-    hipLaunchKernelGGL(preview_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R, accum,
-                       segcount, stats);
+    // the primitive kinds of the scene pick the instance, as for wf_extend_kernel
+    const void *fn = S.has_models ? reinterpret_cast<const void *>(preview_kernel<kPrimsModels>)
+                     : S.has_cuboids ? reinterpret_cast<const void *>(preview_kernel<kPrimsBoxes>)
+                                     : reinterpret_cast<const void *>(preview_kernel<kPrimsSpheres>);
+    void *args[] = {const_cast<DevScene *>(&S), const_cast<DevCamera *>(&C), const_cast<DevRender *>(&R), &accum,
+                    &segcount, &stats};
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth), stream);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

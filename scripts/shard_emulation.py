@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Strong-scaling rehearsal on one GPU: time every shard of an N-way tile split of the bench
+frame (C3, 1920x1080x256 by default) one after the other.  max over shards ~ the N-GPU step
+time without the RCCL gather; sum/ max = the load-balance ceiling of the speed-up.
+Usage: python scripts/shard_emulation.py [--config C3] [--spp 256] [--ns 1 2 4 8]"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
+    args = ap.parse_args()
+    import torch
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
+
+    sc, cam, rs = S.make_config(args.config)
+    if args.spp:
+        rs.spp = args.spp
+    W, H = rs.width, rs.height
+    r = HipRenderer(device=0)
+    r.set_scene(sc)
+    r.set_camera(cam)
+    r.max_depth, r.seed = rs.max_depth, rs.seed
+    out = {"config": args.config, "spp": rs.spp, "runs": {}}
+    stream = torch.cuda.current_stream().cuda_stream
+    for n in args.ns:
+        times, segs = [], []
+        for k in range(n):
+            acc = torch.zeros((shard_pixels(W, H, k, n), 4), dtype=torch.float32, device="cuda")
+            p = r.params(W, H, 0, rs.spp, k, n, compact=True)
+            r.render_device(p, acc.data_ptr(), None, stream)  # warm (allocations)
+            torch.cuda.synchronize()
+            acc.zero_()
+            r.reset_stats()
+            t0 = time.perf_counter()
+            r.render_device(p, acc.data_ptr(), None, stream)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+            segs.append(r.stats()["segments"])
+        t1 = out["runs"].get("1", {}).get("max_ms")
+        mx = max(times) * 1e3
+        out["runs"][str(n)] = {"max_ms": round(mx, 2), "min_ms": round(min(times) * 1e3, 2),
+                               "mean_ms": round(sum(times) / n * 1e3, 2),
+                               "seg_imbalance": round(max(segs) / (sum(segs) / n), 4),
+                               "speedup_vs_1": round(t1 / mx, 3) if t1 else None}
+        print(json.dumps({n: out["runs"][str(n)]}), flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
