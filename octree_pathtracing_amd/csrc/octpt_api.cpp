@@ -713,7 +713,7 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->num_cu = prop.multiProcessorCount;
     ctx->pool_cap = env_u32("OCTPT_POOL", kDefaultPool);
     ctx->chunk_cap = std::min<uint64_t>(env_u32("OCTPT_CHUNK", (uint32_t)kMaxChunkPaths), kMaxChunkPaths);
-    ctx->refill = std::min<uint32_t>(env_u32("OCTPT_REFILL", kDefaultRefill), 64u);
+    ctx->refill = std::max<uint32_t>(std::min<uint32_t>(env_u32("OCTPT_REFILL", kDefaultRefill), 64u), 1u);
     ctx->leaf_batch = std::min<uint32_t>(env_u32("OCTPT_LEAF_BATCH", kDefaultLeafBatch), 64u);
     if (const char *m = std::getenv("OCTPT_EXTEND")) {  // extend variant: "split" = wave-specialised
         if (std::string(m) == "split") ctx->leaf_batch = kLeafSplit;
@@ -789,7 +789,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
             n_slots += (size_t)__builtin_popcount(d->octants[n].child_mask & 0xFFu);
         }
         if (n_slots >= 0xFFFFFFFFull) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree too large");
-        std::vector<uint2> child(std::max<size_t>(n_slots, 1), make_uint2(0u, 0u));
+        // + 8 zero slots: a child index computed for an absent child of the last octant stays in bounds
+        std::vector<uint2> child(n_slots + 8, make_uint2(0u, 0u));
         for (uint32_t n = 0; n < d->octant_count; ++n) {
             const octpt_octant &o = d->octants[n];
             uint32_t k = base[n];

@@ -646,14 +646,13 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     if (cy) E.pos.y = E.pos.y + delta;
     if (cz) E.pos.z = E.pos.z + delta;
     const uint32_t step_mask = (cx ? 1u : 0u) | (cy ? 2u : 0u) | (cz ? 4u : 0u);
-    if (descend) {
-        // level = scale - (OCTREE_MAX_SCALE - depth) = exponent(scale_exp2) - 127 + depth is in
-        // [1, depth): leaf cells (level 0) are never descended from, and a pop always rises at least
-        // one level above them, so level 0 is never written or read and LDS holds levels 1..depth-1
-        // (stack slot = level - 1; the oracle's level-0 entry stays zero, like the miss below)
-        const int slot_i = (int)(__float_as_uint(E.scale_exp2) >> 23) - 128 + (int)S.depth;
-        if (tc_max < E.h && slot_i >= 0) stk_write(stk, (uint32_t)slot_i, E.parent, E.t_max, E.pmask);
-    }
+    // push: level = scale - (OCTREE_MAX_SCALE - depth) = exponent(scale_exp2) - 127 + depth is in
+    // [1, depth) for a descend: leaf cells (level 0) are never descended from, and a pop always rises
+    // at least one level above them, so level 0 is never written or read and LDS holds levels
+    // 1..depth-1 (stack slot = level - 1 >= 0; the oracle's level-0 entry stays zero, like the miss
+    // below).  One guarded write, so that the selects below stay branch-free.
+    const uint32_t slot_u = (__float_as_uint(E.scale_exp2) >> 23) - 128u + S.depth;
+    if (descend && tc_max < E.h) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
     E.h = descend ? tc_max : E.h;
     E.parent = descend ? slot.x : E.parent;  // (octant, its mask)
     E.pmask = descend ? slot.y : E.pmask;
@@ -661,22 +660,24 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     E.t_max = descend ? tv_max : E.t_max;
     E.t_min = descend ? E.t_min : tc_max;
     E.idx = descend ? step_mask : (E.idx ^ step_mask);
+    bool escaped = false;
     if (!descend && (E.idx & step_mask) != 0u) {  // pop (:262-299)
         uint32_t diff = 0u;
         if (step_mask & 1u) diff |= __float_as_uint(E.pos.x) ^ __float_as_uint(E.pos.x + E.scale_exp2);
         if (step_mask & 2u) diff |= __float_as_uint(E.pos.y) ^ __float_as_uint(E.pos.y + E.scale_exp2);
         if (step_mask & 4u) diff |= __float_as_uint(E.pos.z) ^ __float_as_uint(E.pos.z + E.scale_exp2);
-        const uint32_t scale = diff ? 31u - (uint32_t)__clz(diff) : 0xFFFFFFFFu;
-        if (scale >= OCTREE_MAX_SCALE) return kStepMiss;
+        const uint32_t scale_raw = diff ? 31u - (uint32_t)__clz(diff) : 0xFFFFFFFFu;
+        // escaping the root is a miss (:281-283); its lane finishes the block on a clamped scale
+        // and reports the miss at the end, so the pop stays one branch level
+        escaped = scale_raw >= OCTREE_MAX_SCALE;
+        const uint32_t scale = escaped ? OCTREE_MAX_SCALE - 1u : scale_raw;
         E.scale_exp2 = __uint_as_float((scale - OCTREE_MAX_SCALE + 127u) << 23);
-        // slots below the finest level were never written: the oracle reads its zeroed entry
+        // a pop rises above the level it advanced at (the step's own bit, 2^(s-23) in pos's
+        // mantissa, always differs, and the pop condition means a higher one does), so
+        // scale > base = OCTREE_MAX_SCALE - depth and the entry is in the LDS stack (levels 1..)
         const uint32_t base = OCTREE_MAX_SCALE - S.depth;
-        uint2 e = make_uint2(0u, 0u);
-        uint32_t em = S.node0_mask;
-        if (scale > base) {
-            e = stk.e[(scale - base - 1u) * kS];
-            em = stk.m[(scale - base - 1u) * kS];
-        }
+        const uint2 e = stk.e[(scale - base - 1u) * kS];
+        const uint32_t em = stk.m[(scale - base - 1u) * kS];
         E.parent = e.x;
         E.pmask = em;
         E.t_max = __uint_as_float(e.y);
@@ -687,7 +688,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         E.idx = (shx & 1u) | ((shy & 1u) << 1) | ((shz & 1u) << 2);
         E.h = 0.0f;
     }
-    return kStepContinue;
+    return escaped ? kStepMiss : kStepContinue;
 }
 
 // ---------------------------------------------------------------------------
@@ -1434,10 +1435,12 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
     Esvo E;
     uint2 leaf = make_uint2(0u, 0u);
     float t_accept = 0.0f;
-    for (;;) {
+    bool more = true;
+    do {
+        // refill (refill >= 1, clamped by the host): one scalar test per iteration
         const bool idle = !active;
         const uint64_t im = __ballot(idle);
-        if (rays_left && im != 0ull && ((uint32_t)__popcll(im) >= refill || ~im == 0ull)) {
+        if (rays_left && (uint32_t)__popcll(im) >= refill) {
             const uint32_t my = wave_ticket(B.ctrl + ctr_head(q, seg), idle);
             bool dry = false;
             if (idle) {
@@ -1464,7 +1467,26 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
             }
         }
         const uint64_t am = __ballot(active);
-        if (am == 0ull && !rays_left) break;  // (am == 0 with rays left: the next pass refills)
+        // the loop ends after a pass in which no lane was active and no ray was left (with am == 0
+        // the step below does nothing).  Testing it at the bottom, made uniform by readfirstlane,
+        // keeps this a scalar-branch loop instead of an exec-mask loop.
+        more = __builtin_amdgcn_readfirstlane((am != 0ull || rays_left) ? 1u : 0u) != 0u;
+#ifdef OCTPT_INJECT_SALU  // cost experiment: OCTPT_INJECT_SALU extra scalar ALU instructions per iteration
+        {
+            uint32_t sd = __builtin_amdgcn_readfirstlane(pos);
+#pragma unroll
+            for (int k = 0; k < OCTPT_INJECT_SALU; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sd));
+            if (sd == 0xDEADBEEFu) segs_w++;
+        }
+#endif
+#ifdef OCTPT_INJECT_VALU  // cost experiment: OCTPT_INJECT_VALU extra vector ALU instructions per iteration
+        {
+            uint32_t vd = pos;
+#pragma unroll
+            for (int k = 0; k < OCTPT_INJECT_VALU; ++k) asm volatile("v_add_u32 %0, %0, 1" : "+v"(vd));
+            if (vd == 0xDEADBEEFu) cnt.tex++;
+        }
+#endif
         // deferred leaf tests [kStepLeaf]: run once leaf_batch lanes wait, or every active lane does
         const uint64_t pm = kDefer ? __ballot(pend) : 0ull;
         if (pm != 0ull && ((uint32_t)__popcll(pm) >= leaf_batch || pm == am)) {
@@ -1491,7 +1513,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
                 active = false;
             }
         }
-    }
+    } while (more);
     cnt.segs = (threadIdx.x & 63u) == 0u ? segs_w : 0u;  // flush_counters sums over the wave's lanes
     flush_counters(cnt, stats);
 }
