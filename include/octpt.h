@@ -180,7 +180,9 @@ typedef struct octpt_render_params {
     uint32_t width, height;
     uint32_t spp_start, spp_count;
     uint32_t max_depth;    /* reference: 5 (path_tracer.rs:56) */
-    uint32_t branch_count; /* only 1 is supported (SURVEY contract C6) */
+    uint32_t branch_count; /* TileRenderer branch count B <= 64: passes of weight
+                            * get_current_branch_count(spp, B), the first reflection split into that many
+                            * branches; spp_start and spp_start + spp_count must be pass boundaries */
     uint32_t seed;
     uint32_t shard_index, shard_count; /* 8x8 tile t belongs to shard t % shard_count */
     uint32_t flags;

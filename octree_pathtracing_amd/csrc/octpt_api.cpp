@@ -67,6 +67,10 @@ struct octpt_ctx {
     DevCamera C{};
     // per-context device state
     uint32_t *d_counters = nullptr;  // ring of work counters, one per launch
+    // branch schedule of the current render (C20): host copy + grow-only device table
+    std::vector<uint2> h_subs;
+    uint2 *d_subs = nullptr;
+    size_t subs_cap = 0;
     uint32_t launch_seq = 0;
     unsigned long long *d_stats = nullptr;
     uint8_t *d_lut_byte = nullptr;
@@ -358,8 +362,8 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     if (p->width == 0 || p->height == 0 || (uint64_t)p->width * p->height >= (1ull << 31))
         return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad resolution");
     if (p->max_depth == 0) return fail(ctx, OCTPT_ERR_INVALID_ARG, "max_depth must be >= 1");
-    if (p->branch_count > 1)
-        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "branch_count > 1 is not implemented (SURVEY contract C6)");
+    const uint32_t B = p->branch_count ? p->branch_count : 1u;
+    if (B > 64u) return fail(ctx, OCTPT_ERR_INVALID_ARG, "branch_count must be <= 64");
     if (p->shard_count == 0 || p->shard_index >= p->shard_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad shard");
     if ((uint64_t)p->spp_start + p->spp_count >= (1ull << 24))
         return fail(ctx, OCTPT_ERR_INVALID_ARG, "spp_start + spp_count must stay below 2^24");
@@ -378,6 +382,38 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     R.shard_tiles = tiles_of_shard(R.tiles_x * tiles_y, p->shard_index, p->shard_count);
     R.total_items = R.shard_tiles * 64u;
     R.dim = (float)std::max(p->width, p->height);
+    R.subs = nullptr;
+    if (B > 1u && !(p->flags & OCTPT_RENDER_PREVIEW)) {
+        // TileRenderer pass schedule (tile_renderer.rs:416-484, C20): the call covers whole passes
+        if (p->flags & OCTPT_RENDER_MEGAKERNEL)
+            return fail(ctx, OCTPT_ERR_UNSUPPORTED, "branch_count > 1 runs on the wavefront path only");
+        uint64_t spp = 0;
+        while (spp < p->spp_start) spp += current_branch_count((uint32_t)spp, B);
+        if (spp != p->spp_start)
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "spp_start is not a pass boundary of the branch schedule");
+        const uint64_t end = (uint64_t)p->spp_start + p->spp_count;
+        ctx->h_subs.clear();
+        while (spp < end) {
+            const uint32_t bc = current_branch_count((uint32_t)spp, B);
+            for (uint32_t b = 0; b < bc; ++b) ctx->h_subs.push_back(make_uint2((uint32_t)spp, bc | (b << 16)));
+            spp += bc;
+        }
+        if (spp != end)
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "spp_start + spp_count is not a pass boundary of the branch schedule");
+        if (!ctx->h_subs.empty()) {
+            HIP_TRY(ctx, hipDeviceSynchronize());  // an earlier render may still read the table
+            if (ctx->h_subs.size() > ctx->subs_cap) {
+                if (ctx->d_subs) (void)hipFree(ctx->d_subs);
+                ctx->d_subs = nullptr;
+                ctx->subs_cap = 0;
+                HIP_TRY(ctx, hipMalloc(&ctx->d_subs, ctx->h_subs.size() * sizeof(uint2)));
+                ctx->subs_cap = ctx->h_subs.size();
+            }
+            HIP_TRY(ctx, hipMemcpy(ctx->d_subs, ctx->h_subs.data(), ctx->h_subs.size() * sizeof(uint2),
+                                   hipMemcpyHostToDevice));
+            R.subs = ctx->d_subs;
+        }
+    }
     // RendererMode::Preview renders one replacing pass; spp and max_depth do not apply (C16)
     R.preview = (p->flags & OCTPT_RENDER_PREVIEW) ? 1u : 0u;
     if (R.preview) R.spp_count = 1u;
@@ -501,7 +537,9 @@ octpt_status enqueue_megakernel(octpt_ctx *ctx, const DevRender &R, float4 *d_ac
 octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s,
                                const std::atomic<bool> *cancel) {
     const uint64_t n_px = R.total_items;
-    const uint32_t chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, ctx->chunk_cap / n_px));
+    uint32_t chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, ctx->chunk_cap / n_px));
+    // a branch-schedule chunk holds whole passes (<= 64 sub-samples each, C20)
+    if (R.subs) chunk_spp = std::max(chunk_spp, std::min(64u, R.spp_count));
     const uint64_t chunk_max = (uint64_t)chunk_spp * n_px;
     const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
     octpt_status st = ensure_wave(ctx, pool, chunk_max, ctx->S.sun.sun_sampling != 0);
@@ -516,10 +554,21 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const int seg_blocks = (int)(kSegs * 64u / kBlock);
     const int grid_shade = (ctx->num_cu * 4 + seg_blocks - 1) / seg_blocks * seg_blocks;
     const WaveBuffers &B = ctx->wb;
-    for (uint32_t c0 = 0; c0 < R.spp_count; c0 += chunk_spp) {
+    for (uint32_t c0 = 0, c1 = 0; c0 < R.spp_count; c0 = c1) {
+        c1 = c0 + std::min(chunk_spp, R.spp_count - c0);
+        if (R.subs) {  // a chunk ends on a pass boundary (C20): branches of one pass resolve together
+            uint32_t e = c1;
+            while (e < R.spp_count && (ctx->h_subs[e].y >> 16) != 0u) --e;
+            if (e <= c0) {  // one pass larger than the chunk: take the whole pass
+                e = c1;
+                while (e < R.spp_count && (ctx->h_subs[e].y >> 16) != 0u) ++e;
+            }
+            c1 = e;
+        }
         DevRender Rc = R;
         Rc.spp_start = R.spp_start + c0;
-        Rc.spp_count = std::min(chunk_spp, R.spp_count - c0);
+        Rc.spp_count = c1 - c0;
+        if (R.subs) Rc.subs = R.subs + c0;
         const uint32_t chunk_items = (uint32_t)((uint64_t)Rc.spp_count * n_px);
         HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, kCtrlWords * sizeof(uint32_t), s));
         const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
@@ -760,6 +809,7 @@ void octpt_destroy(octpt_ctx *ctx) {
     for (auto &ev : ctx->count_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_subs) (void)hipFree(ctx->d_subs);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_lut_float) (void)hipFree(ctx->d_lut_float);
     if (ctx->d_lut_byte) (void)hipFree(ctx->d_lut_byte);

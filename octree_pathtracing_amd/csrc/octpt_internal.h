@@ -119,7 +119,19 @@ struct DevRender {
     uint32_t total_items;    // shard_tiles * 64 work items
     float dim;               // max(W, H)
     uint32_t preview;        // RendererMode::Preview
+    // branch schedule, NULL when branch_count == 1: sub-sample k of this call is
+    // subs[k] = (pass spp, pass branch count | branch << 16); spp_count then counts sub-samples
+    const uint2 *subs;
 };
+
+// TileRenderer::get_current_branch_count (tile_renderer.rs:196-206)
+inline uint32_t current_branch_count(uint32_t current_spp, uint32_t scene_branch_count) {
+    if (current_spp < scene_branch_count) {
+        if (current_spp <= (uint32_t)sqrtf((float)scene_branch_count)) return 1u;
+        return scene_branch_count - current_spp;
+    }
+    return scene_branch_count;
+}
 
 // wavefront path tracer state.
 // A single device-scope counter sustains only ~88 M atomicAdd/s on MI355X (tools/atomic_bench.hip),

@@ -168,6 +168,11 @@ __device__ __forceinline__ float rng_next(uint32_t &st) {
     return (float)(w >> 8) * (1.0f / 16777216.0f);
 }
 
+// RNG stream of branch b > 0 of a split first reflection
+__device__ __forceinline__ uint32_t branch_state(uint32_t state, uint32_t b) {
+    return lowbias32(state ^ (b * 0x632BE5ABu));
+}
+
 // ---------------------------------------------------------------------------
 // rays, path state, counters
 // ---------------------------------------------------------------------------
@@ -197,6 +202,8 @@ struct PathState {
     v3 T, L;
     uint32_t cur, prev, depth, last_prim, path_segs, rng;
     bool specular;
+    uint32_t branch;    // branch of a split first reflection (C20), 0 = the path's own stream
+    uint32_t seg_base;  // branch > 0: the segments replayed before the split (not reported)
     // next-event estimation (sun sampling), used by the kNee instances only: while
     // `shadow` is set the ray is a get_direct_light_attenuation segment carrying `att`; the diffuse
     // bounce it interrupts waits in (co, cd, cn, clast, ccur), `mult` = |d_sun . n| * lum_a
@@ -876,6 +883,8 @@ __device__ inline void new_path(const DevCamera &C, const DevRender &R, uint32_t
     ps.path_segs = 0u;
     ps.specular = true;
     ps.shadow = false;
+    ps.branch = 0u;
+    ps.seg_base = 0u;
 }
 
 // next_intersection prologue (path_tracer.rs:438-446) + Scene::hit direction guard
@@ -950,6 +959,10 @@ __device__ inline bool shade_segment(const DevScene &S, const DevRender &R, Path
     }
     if (ray.depth + 1u >= R.max_depth) return false;
     ray.depth += 1u;
+    if (ray.depth == 1u && ray.branch != 0u) {  // the first reflection splits (path_tracer.rs:66) [C20]
+        ray.rng = branch_state(ray.rng, ray.branch);
+        ray.seg_base = ray.path_segs;
+    }
     cnt.shade++;
     v3 &T = ray.T;
     const float metal = m.metalness;
@@ -1038,13 +1051,13 @@ __device__ inline bool shade_segment(const DevScene &S, const DevRender &R, Path
     return true;
 }
 
-// running mean of render_tile_average (tile_renderer.rs:716-733), branch_count = 1
-__device__ __forceinline__ void running_mean(float4 &fb, v3 c, uint32_t spp) {
-    const float s_inv = 1.0f / (float)(1u + spp);
-    const float fs = (float)spp;
-    fb.x = (fb.x * fs + c.x * 1.0f) * s_inv;
-    fb.y = (fb.y * fs + c.y * 1.0f) * s_inv;
-    fb.z = (fb.z * fs + c.z * 1.0f) * s_inv;
+// running mean of render_tile_average (tile_renderer.rs:707-733): a sample of weight bc
+__device__ __forceinline__ void running_mean(float4 &fb, v3 c, uint32_t spp, uint32_t bc) {
+    const float s_inv = 1.0f / (float)(bc + spp);
+    const float fs = (float)spp, w = (float)bc;
+    fb.x = (fb.x * fs + c.x * w) * s_inv;
+    fb.y = (fb.y * fs + c.y * w) * s_inv;
+    fb.z = (fb.z * fs + c.z * w) * s_inv;
 }
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
@@ -1173,7 +1186,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             if (cont) {
                 state = ST_BEGIN;
             } else {
-                running_mean(fb, ray.L, R.spp_start + k);
+                running_mean(fb, ray.L, R.spp_start + k, 1u);
                 k++;
                 if (k < R.spp_count) {
                     state = ST_NEWPATH;
@@ -1284,7 +1297,7 @@ __device__ __forceinline__ void store_path(const WaveBuffers &B, uint32_t slot, 
     B.pa[slot] = make_float4(ps.T.x, ps.T.y, ps.T.z, ps.L.x);
     B.pb[slot] = make_float4(ps.L.y, ps.L.z, __uint_as_float(ps.rng), __uint_as_float(item));
     B.pc[slot] = make_uint2(ps.cur, ps.depth | (ps.specular ? 1u << 8 : 0u) | (ps.shadow ? 1u << 9 : 0u) |
-                                        (ps.path_segs << 16));
+                                        (ps.branch << 10) | (ps.path_segs << 16) | (ps.seg_base << 23));
 }
 
 // sun-sampling state of a slot (kNee): the waiting bounce + mult, and the attenuation
@@ -1323,7 +1336,9 @@ __device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, f
     ps.depth = c.y & 255u;
     ps.specular = (c.y >> 8) & 1u;
     ps.shadow = (c.y >> 9) & 1u;
-    ps.path_segs = c.y >> 16;
+    ps.branch = (c.y >> 10) & 63u;
+    ps.path_segs = (c.y >> 16) & 127u;
+    ps.seg_base = c.y >> 23;
 }
 
 // generate the path of chunk item `item` into `slot`; false when the pixel lies outside the image
@@ -1336,7 +1351,14 @@ __device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const W
         B.color[item] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         return false;
     }
-    new_path(C, R, y * R.W + x, R.spp_start + s_local, ps);
+    uint32_t sample = R.spp_start + s_local, branch = 0u;
+    if (R.subs) {  // branch schedule (C20): the pass's sample key and this item's branch
+        const uint2 sb = R.subs[s_local];
+        sample = sb.x;
+        branch = sb.y >> 16;
+    }
+    new_path(C, R, y * R.W + x, sample, ps);
+    ps.branch = branch;
     begin_segment(ps);  // first segment: never capped
     cnt.paths++;
     store_path(B, slot, ps, item);
@@ -1859,7 +1881,11 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
                 }
                 append = true;
             } else {
-                B.color[item] = make_float4(ps.L.x, ps.L.y, ps.L.z, __uint_as_float(ps.path_segs));
+                // segments this item reports (a branch > 0 reports none of the replayed prefix) and
+                // whether the first reflection split (C20)
+                const uint32_t segs = ps.branch == 0u ? ps.path_segs : (ps.depth ? ps.path_segs - ps.seg_base : 0u);
+                B.color[item] = make_float4(ps.L.x, ps.L.y, ps.L.z,
+                                            __uint_as_float(segs | (ps.depth ? 0x80000000u : 0u)));
                 finished = true;
             }
         }
@@ -1882,10 +1908,31 @@ __global__ __launch_bounds__(kBlock) void wf_resolve_kernel(DevRender R, WaveBuf
     const uint32_t acc_idx = R.compact ? px_item : y * R.W + x;
     float4 fb = accum[acc_idx];
     uint32_t segs = 0u;
+    v3 L0 = V(0.0f, 0.0f, 0.0f), sum = L0;
+    bool split = false;
     for (uint32_t s = 0; s < chunk_spp; ++s) {
         const float4 c = B.color[(size_t)s * R.total_items + px_item];
-        running_mean(fb, V(c.x, c.y, c.z), R.spp_start + s);
-        segs += __float_as_uint(c.w);
+        const uint32_t w = __float_as_uint(c.w);
+        segs += w & 0x7FFFFFFFu;
+        if (!R.subs) {
+            running_mean(fb, V(c.x, c.y, c.z), R.spp_start + s, 1u);
+            continue;
+        }
+        // branch schedule (C20): a pass's branches fold into one sample of weight bc; the colour
+        // is their mean when the first reflection split, else branch 0's (all branches agree)
+        const uint2 sb = R.subs[s];
+        const uint32_t b = sb.y >> 16, bc = sb.y & 0xFFFFu;
+        if (b == 0u) {
+            L0 = V(c.x, c.y, c.z);
+            sum = vadd(V(0.0f, 0.0f, 0.0f), L0);
+            split = (w >> 31) != 0u;
+        } else {
+            sum = vadd(sum, V(c.x, c.y, c.z));
+        }
+        if (b + 1u == bc) {
+            const float inv = 1.0f / (float)bc;
+            running_mean(fb, split ? vscale(sum, inv) : L0, sb.x, bc);
+        }
     }
     accum[acc_idx] = fb;
     if (segcount) segcount[acc_idx] += segs;

@@ -97,6 +97,7 @@ class HipRenderer:
         self.target_spp = target_spp
         self.seed = seed
         self.max_depth = max_depth
+        self.branch_count = 1  # TileRenderer branch count; 1 = one path per sample
         self._scene_keep = None
         self._accum = None
         self._spp = 0
@@ -175,6 +176,8 @@ class HipRenderer:
             self._accum[..., 3] = 1.0
         preview = self._mode is RendererMode.Preview
         n = spp_count if spp_count is not None else max(self.target_spp - self._spp, 1)
+        if self.branch_count > 1:  # whole passes of the branch schedule (C20), as TileRenderer runs them
+            n = branch_pass_end(self._spp, n, self.branch_count) - self._spp
         if preview:  # render_preview (tile_renderer.rs:339-374): one replacing pass, current_spp stays 0
             n = 0
         p = self.params(W, H, self._spp, n, preview=preview)
@@ -212,8 +215,8 @@ class HipRenderer:
                megakernel=False, kernel_timing=False, preview=False) -> "_lib.RenderParams":
         flags = ((_lib.RENDER_SHARD_COMPACT if compact else 0) | (_lib.RENDER_MEGAKERNEL if megakernel else 0)
                  | (_lib.RENDER_KERNEL_TIMING if kernel_timing else 0) | (_lib.RENDER_PREVIEW if preview else 0))
-        return _lib.RenderParams(W, H, spp_start, spp_count, self.max_depth, 1, self.seed, shard_index, shard_count,
-                                 flags)
+        return _lib.RenderParams(W, H, spp_start, spp_count, self.max_depth, self.branch_count, self.seed,
+                                 shard_index, shard_count, flags)
 
     def render(self, settings: RenderSettings, accum: np.ndarray | None = None, spp_start: int = 0,
                with_rgba: bool = False):
@@ -270,6 +273,23 @@ class HipRenderer:
 
     def reset_stats(self) -> None:
         self._check(self._lib.octpt_reset_stats(self._ctx))
+
+
+def current_branch_count(current_spp: int, scene_branch_count: int) -> int:
+    """TileRenderer::get_current_branch_count (tile_renderer.rs:196-206), f32 square root."""
+    if current_spp < scene_branch_count:
+        if current_spp <= int(np.sqrt(np.float32(scene_branch_count))):
+            return 1
+        return scene_branch_count - current_spp
+    return scene_branch_count
+
+
+def branch_pass_end(spp_start: int, spp_count: int, scene_branch_count: int) -> int:
+    """The first pass boundary of the branch schedule at or after spp_start + spp_count (C20)."""
+    spp = 0
+    while spp < spp_start + spp_count:
+        spp += current_branch_count(spp, scene_branch_count)
+    return spp
 
 
 def shard_pixels(W: int, H: int, shard_index: int, shard_count: int) -> int:

@@ -259,6 +259,19 @@ static void lut_init(void) {
 float ref_lut_float(uint32_t i) { pthread_once(&lut_once, lut_init); return LUT_FLOAT[i & 255]; }
 uint8_t ref_lut_byte(uint32_t i) { pthread_once(&lut_once, lut_init); return LUT_BYTE[i & 255]; }
 
+/* TileRenderer::get_current_branch_count (tile_renderer.rs:196-206) [C20] */
+uint32_t ref_branch_count(uint32_t current_spp, uint32_t scene_branch_count) {
+    if (current_spp < scene_branch_count) {
+        if (current_spp <= (uint32_t)sqrtf((float)scene_branch_count)) return 1;
+        return scene_branch_count - current_spp;
+    }
+    return scene_branch_count;
+}
+
+/* RNG stream of branch b > 0 of a split path [C20]: a lowbias32 hash of the stream state at the
+ * split and the branch index */
+uint32_t ref_rng_branch_state(uint32_t state, uint32_t b) { return lowbias32(state ^ (b * 0x632BE5ABu)); }
+
 /* ------------------------------------------------------------------------- */
 /* scene-derived constants: Sun::new (scene/mod.rs:321-383)                     */
 /* ------------------------------------------------------------------------- */
@@ -284,7 +297,8 @@ typedef struct {
     const ref_scene *s;
     sun_k sun;
     float octree_scale;
-    uint32_t max_depth, branch_count;
+    uint32_t max_depth, branch_count; /* branch_count: the schedule's ceiling B [C20] */
+    uint32_t cur_bc;                  /* this pass's branch count get_current_branch_count(spp, B) */
     int forward;
     uint32_t path_segs; /* next_intersection calls of the current path [C15] */
     ref_stats st;
@@ -1152,8 +1166,22 @@ static int path_trace(ctx_t *c, ray_t *ray, int first, uint32_t *rng, fwd_t *fw,
         ray_t next;
         memset(&next, 0, sizeof next);
         float metal = cur->metalness;
-        uint32_t count = first ? c->branch_count : 1;
+        /* the first reflection splits into branch_count branches (:66, [C20]): each branch starts
+         * from the same hit record, the same path-segment count [C15] and forward state, branch 0
+         * continues the path's RNG stream and branch b > 0 draws from branch_state(stream, b) */
+        uint32_t count = first ? c->cur_bc : 1;
+        uint32_t rng0 = *rng, ps0 = c->path_segs;
+        float col0[4], Lsum[3] = {0.0f, 0.0f, 0.0f};
+        fwd_t fw0;
+        memcpy(col0, ray->col, sizeof col0);
+        if (fw) fw0 = *fw;
         for (uint32_t b = 0; b < count; b++) {
+            if (first && b > 0) {
+                *rng = ref_rng_branch_state(rng0, b);
+                c->path_segs = ps0;
+                memcpy(ray->col, col0, sizeof col0);
+                if (fw) *fw = fw0;
+            }
             int do_metal = metal > RAY_EPSILON && ref_rng_next(rng) < metal;
             if (do_metal || (specular > RAY_EPSILON && ref_rng_next(rng) < specular))
                 hit |= do_specular_reflection(c, ray, &next, cum, do_metal, rng, fw, segs);
@@ -1163,9 +1191,11 @@ static int path_trace(ctx_t *c, ray_t *ray, int first, uint32_t *rng, fwd_t *fw,
                 hit |= do_refraction(c, ray, &next, cur, cum, ior1, ior2, absorb, rng, fw, segs);
             else
                 hit |= do_transmission(c, ray, &next, cum, absorb, rng, fw, segs);
+            if (first && fw) for (int i = 0; i < 3; i++) Lsum[i] += fw->L[i];
         }
         float inv = 1.0f / (float)count;
         for (int i = 0; i < 4; i++) ray->col[i] = cum[i] * inv;
+        if (first && fw) for (int i = 0; i < 3; i++) fw->L[i] = Lsum[i] * inv;
         break;
     }
     if (!hit) {
@@ -1258,8 +1288,11 @@ static void render_rows(job_t *j, ctx_t *c) {
             uint32_t pix = y * W + x;
             float *fb = &j->accum[4 * (size_t)pix];
             uint32_t segs = 0;
-            for (uint32_t k = 0; k < p->spp_count; k++) {
-                uint32_t spp = p->spp_start + k * c->branch_count;
+            /* TileRenderer passes (tile_renderer.rs:416-484) [C20]: pass weight bc from the schedule,
+             * the sample keyed by the accumulated spp at the pass start, until spp_start + spp_count */
+            for (uint32_t spp = p->spp_start; spp < p->spp_start + p->spp_count;) {
+                uint32_t bc = ref_branch_count(spp, c->branch_count);
+                c->cur_bc = bc;
                 uint32_t rng = ref_rng_path_state(p->seed, pix, spp);
                 float xn = ((float)(2 * x + 1) - (float)W) / dim;
                 float yn = ((float)(2 * (H - y) - 1) - (float)H) / dim;
@@ -1281,9 +1314,9 @@ static void render_rows(job_t *j, ctx_t *c) {
                     path_trace(c, &ray, 1, &rng, NULL, &segs);
                     memcpy(col, ray.col, sizeof col);
                 }
-                float bc = (float)c->branch_count;
-                float s_inv = 1.0f / (float)(c->branch_count + spp);
-                for (int i = 0; i < 3; i++) fb[i] = (fb[i] * (float)spp + col[i] * bc) * s_inv;
+                float s_inv = 1.0f / (float)(bc + spp); /* render_tile_average :707-731 */
+                for (int i = 0; i < 3; i++) fb[i] = (fb[i] * (float)spp + col[i] * (float)bc) * s_inv;
+                spp += bc;
             }
             if (j->seg_count) j->seg_count[pix] = segs;
         }
@@ -1299,7 +1332,7 @@ static void *render_worker(void *arg) {
     c.octree_scale = ldexpf(1.0f, -(int)j->s->depth);
     c.max_depth = j->p->max_depth;
     c.branch_count = j->p->branch_count ? j->p->branch_count : 1;
-    c.forward = j->p->forward_accumulation && c.branch_count == 1;
+    c.forward = j->p->forward_accumulation;
     if (j->p->preview) preview_rows(j, &c);
     else render_rows(j, &c);
     pthread_mutex_lock(&j->lock);

@@ -135,6 +135,8 @@ float ref_math_acos(float x);
 float ref_math_atan2(float y, float x);
 float ref_math_hypot(float x, float y);
 uint32_t ref_rng_path_state(uint32_t seed, uint32_t pixel, uint32_t sample);
+uint32_t ref_rng_branch_state(uint32_t state, uint32_t b);
+uint32_t ref_branch_count(uint32_t current_spp, uint32_t scene_branch_count);
 float ref_rng_next(uint32_t *state);
 
 /* --- Morton, reference new_octree.rs:752-835 --- */

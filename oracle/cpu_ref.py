@@ -118,6 +118,10 @@ def load() -> C.CDLL:
     lib.ref_intersect_brute.argtypes = [C.POINTER(RefScene), vp, u32, vp, vp]
     lib.ref_quad_hit.restype = None
     lib.ref_quad_hit.argtypes = [vp, vp, vp, u32, vp, vp]
+    lib.ref_branch_count.restype = u32
+    lib.ref_branch_count.argtypes = [u32, u32]
+    lib.ref_rng_branch_state.restype = u32
+    lib.ref_rng_branch_state.argtypes = [u32, u32]
     lib.ref_render.restype = C.c_int
     lib.ref_render.argtypes = [C.POINTER(RefScene), C.POINTER(RefCamera), C.POINTER(RefParams), vp, vp,
                                C.POINTER(RefStats)]

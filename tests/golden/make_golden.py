@@ -38,6 +38,9 @@ RENDERS = {
     "c2_hq": ("C2", 160, 90, 2, None, "hq"),
     "c4_hq_sss": ("C4", 64, 36, 2, None, "hq_sss"),
     "c5_nee_importance": ("C5", 96, 54, 2, None, "nee_importance"),
+    # TileRenderer branch count 10: spp 0..20 = passes of weight 1, 1, 1, 1, 6, 10
+    "tiny_branch10": ("tiny", 64, 48, 20, None, {"branch_count": 10}),
+    "blocks_branch10": ("blocks", 48, 36, 20, None, {"branch_count": 10, "variant": "fast"}),
 }
 # RendererMode::Preview fixtures: name -> (config, width, height)
 PREVIEWS = {
@@ -49,16 +52,19 @@ PREVIEWS = {
 
 
 def render_fixture(name):
-    cfg, W, H, spp, md, *variant = RENDERS[name]
+    cfg, W, H, spp, md, *extra = RENDERS[name]
+    opts = extra[0] if extra and isinstance(extra[0], dict) else {"variant": extra[0]} if extra else {}
+    variant, bc = opts.get("variant"), opts.get("branch_count", 1)
     sc, cam, rs = S.make_config(cfg)
     if variant:
-        S.with_sun_variant(sc, variant[0])
+        S.with_sun_variant(sc, variant)
     acc, seg, st = cpu_ref.render(sc, cam, W, H, spp, max_depth=md or rs.max_depth, seed=rs.seed, forward=True,
-                                  threads=8)
+                                  threads=8, branch_count=bc)
     return dict(accum=acc, segcount=seg, stats=np.array([st[k] for k in STAT_KEYS], np.uint64),
                 meta=np.array(json.dumps(dict(config=cfg, width=W, height=H, spp=spp,
                                               max_depth=md or rs.max_depth, seed=rs.seed, forward=True,
-                                              **(dict(sun_variant=variant[0]) if variant else {})))))
+                                              **(dict(sun_variant=variant) if variant else {}),
+                                              **(dict(branch_count=bc) if bc != 1 else {})))))
 
 
 def preview_fixture(name):

@@ -12,7 +12,8 @@ from octree_pathtracing_amd import scene as S
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
 RENDERS = ["c1_as_is", "c1", "tiny", "c2_small", "c3_small", "c4_small", "c5_small", "c3_preview", "c4_preview",
-           "c5_preview", "tiny_fast", "c2_hq", "c4_hq_sss", "c5_nee_importance", "blocks_small", "blocks_preview"]
+           "c5_preview", "tiny_fast", "c2_hq", "c4_hq_sss", "c5_nee_importance", "blocks_small", "blocks_preview", "tiny_branch10",
+           "blocks_branch10"]
 STAT_KEYS = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
              "texel_reads", "max_path_segs")
 
@@ -29,7 +30,8 @@ def test_oracle_reproduces_render_fixture(name):
     if "sun_variant" in m:
         S.with_sun_variant(sc, m["sun_variant"])
     acc, seg, st = cpu_ref.render(sc, cam, m["width"], m["height"], m["spp"], max_depth=m["max_depth"],
-                                  seed=m["seed"], forward=m["forward"], threads=8, preview=m.get("preview", False))
+                                  seed=m["seed"], forward=m["forward"], threads=8, preview=m.get("preview", False),
+                                  branch_count=m.get("branch_count", 1))
     assert np.array_equal(seg, g["segcount"])
     assert np.array_equal(acc, g["accum"])
     assert [st[k] for k in STAT_KEYS] == g["stats"].tolist()

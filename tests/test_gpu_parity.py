@@ -39,13 +39,14 @@ def rel_err(a, b):
 
 
 def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), compact=False, megakernel=False,
-               preview=False):
+               preview=False, branch_count=1):
     """Device render through octpt_render_device; returns (accum[H,W,4] or compact, seg_count, stats)."""
     from octree_pathtracing_amd.renderer import shard_pixels
 
     r.set_scene(sc)
     r.set_camera(cam)
     r.max_depth, r.seed = rs.max_depth, rs.seed
+    r.branch_count = branch_count
     r.reset_stats()
     W, H = rs.width, rs.height
     n = shard_pixels(W, H, *shard) if compact else W * H
@@ -242,12 +243,7 @@ def test_validation_errors(renderer):
         with pytest.raises(_lib.OctptError) as e:
             renderer.set_scene(blk)
         assert e.value.status == _lib.ERR_INVALID_ARG, fault
-    renderer.set_scene(sc)
-    p = renderer.params(rs.width, rs.height, 0, 1)
-    p.branch_count = 10
-    acc = np.zeros((rs.height, rs.width, 4), np.float32)
-    st = renderer._lib.octpt_render(renderer._ctx, C.byref(p), acc.ctypes.data_as(C.c_void_p), None)
-    assert st == _lib.ERR_UNSUPPORTED
+    renderer.set_scene(sc)  # branch-count validation: test_branch_count_validation
 
 
 @pytest.mark.parametrize("case", ["one_pixel", "ragged", "empty_scene", "inside_sphere", "glass_only",
@@ -380,11 +376,16 @@ def test_render_matches_golden_fixture(torch_cuda, renderer, name):
     if "sun_variant" in m:
         S.with_sun_variant(sc, m["sun_variant"])
     rs.width, rs.height, rs.spp, rs.max_depth, rs.seed = m["width"], m["height"], m["spp"], m["max_depth"], m["seed"]
-    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs, preview=m.get("preview", False))
+    bc = m.get("branch_count", 1)
+    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs, preview=m.get("preview", False), branch_count=bc)
     keys = ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests", "leaf_visits", "shade_events",
             "texel_reads", "max_path_segs")
     ref = dict(zip(keys, g["stats"].tolist()))
     assert np.array_equal(segs, g["segcount"])
+    if bc > 1:  # GPU totals also count the replayed camera rays of branches > 0 (C20)
+        e = rel_err(acc, g["accum"])
+        assert e.max() <= REL_TOL_FORWARD, (name, e.max())
+        return
     assert st["segments"] == ref["segments"] and st["esvo_steps"] == ref["esvo_steps"]
     assert st["sphere_tests"] + st["cuboid_tests"] == ref["prim_tests"]
     assert st["shade_events"] == ref["shade_events"] and st["paths"] == ref["paths"]
@@ -573,3 +574,82 @@ def test_sun_sampling_megakernel_and_small_pool(torch_cuda, renderer, variant):
     finally:
         del os.environ["OCTPT_POOL"], os.environ["OCTPT_REFILL"], os.environ["OCTPT_CHUNK"]
     assert np.array_equal(a[0], c[0]) and np.array_equal(a[1], c[1])
+
+
+# ---------------------------------------------------------------------------------------------
+# TileRenderer branch count (DESIGN.md C20): the first reflection splits into branch_count branches,
+# each branch a wavefront path of its own (the camera ray replayed), folded per pass in resolve
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name,res,variant", [("tiny", (64, 48, 20), None), ("C2", (160, 90, 20), None),
+                                              ("blocks", (64, 48, 20), "fast"), ("C4", (96, 54, 10), None)])
+def test_branch_count_parity(torch_cuda, renderer, name, res, variant):
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config(name)
+    if variant:
+        S.with_sun_variant(sc, variant)
+    rs.width, rs.height, rs.spp = res
+    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs, branch_count=10)
+    racc, rsegs, rst = oracle(sc, cam, rs, forward=True, branch_count=10)
+    assert np.array_equal(segs, rsegs), f"{name}: segment counts differ at {np.argwhere(segs != rsegs)[:5]}"
+    assert st["paths"] >= rst["paths"] and st["segments"] >= rst["segments"]
+    e = rel_err(acc, racc)
+    assert e.max() <= REL_TOL_FORWARD, f"{name}: max rel err {e.max()}"
+    assert (acc == racc).mean() > 0.999
+    rec = oracle(sc, cam, rs, forward=False, branch_count=10)
+    assert rel_err(acc, rec[0]).max() <= REL_TOL_RECURSIVE
+
+
+def test_branch_count_progressive_and_chunked(torch_cuda, renderer):
+    """[0, 10) + [10, 40) == [0, 40) on the GPU, and == a render chunked into pass-aligned chunks
+    of a 100-slot pool (OCTPT_CHUNK, OCTPT_POOL)."""
+    import os
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    sc, cam, rs = S.make_config("tiny")
+    rs.width, rs.height, rs.spp = 37, 19, 40
+    whole = gpu_render(torch_cuda, renderer, sc, cam, rs, branch_count=10)
+    rs.spp = 10
+    a = gpu_render(torch_cuda, renderer, sc, cam, rs, branch_count=10)
+    rs.spp = 30
+    b = gpu_render(torch_cuda, renderer, sc, cam, rs, spp_start=10, accum=a[0], branch_count=10)
+    assert np.array_equal(whole[0], b[0]) and np.array_equal(whole[1], a[1] + b[1])
+    # 100 spp = passes 1, 1, 1, 1, 6, 10 x 9; a 65-sub-sample chunk cap (960 tile pixels) makes the
+    # host pull the first chunk back to the pass boundary at 60
+    rs.spp = 100
+    full = gpu_render(torch_cuda, renderer, sc, cam, rs, branch_count=10)
+    os.environ.update({"OCTPT_POOL": "100", "OCTPT_CHUNK": str(65 * 960)})
+    try:
+        small = HipRenderer(0)
+        c = gpu_render(torch_cuda, small, sc, cam, rs, branch_count=10)
+        small.close()
+    finally:
+        del os.environ["OCTPT_POOL"], os.environ["OCTPT_CHUNK"]
+    assert np.array_equal(full[0], c[0]) and np.array_equal(full[1], c[1])
+
+
+def test_branch_count_validation(renderer):
+    from octree_pathtracing_amd import _lib
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config("tiny")
+    renderer.set_scene(sc)
+    renderer.set_camera(cam)
+    acc = np.zeros((rs.height, rs.width, 4), np.float32)
+    renderer.branch_count = 10
+    try:
+        for start, count, flags, want in [(0, 5, 0, _lib.ERR_INVALID_ARG),   # 5 is inside the 6-pass [4, 10)
+                                          (5, 5, 0, _lib.ERR_INVALID_ARG),   # 5 is not a pass start
+                                          (0, 10, _lib.RENDER_MEGAKERNEL, _lib.ERR_UNSUPPORTED),
+                                          (0, 10, 0, _lib.OK)]:
+            p = renderer.params(rs.width, rs.height, start, count)
+            p.flags = flags
+            st = renderer._lib.octpt_render(renderer._ctx, C.byref(p), acc.ctypes.data_as(C.c_void_p), None)
+            assert st == want, (start, count, flags, st)
+        p = renderer.params(rs.width, rs.height, 0, 10)
+        p.branch_count = 65
+        st = renderer._lib.octpt_render(renderer._ctx, C.byref(p), acc.ctypes.data_as(C.c_void_p), None)
+        assert st == _lib.ERR_INVALID_ARG
+    finally:
+        renderer.branch_count = 1
