@@ -857,6 +857,25 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
                 }
             }
         }
+        // single-sphere leaf slots carry their sphere in a parallel array, so that extend loads it
+        // beside the slot instead of after it (sphere-only scenes)
+        std::vector<float4> leaf_sph;
+        if (!d->cuboid_count) {
+            leaf_sph.assign(child.size(), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+            for (uint32_t n = 0; n < d->octant_count; ++n) {
+                const octpt_octant &o = d->octants[n];
+                uint32_t k = base[n];
+                for (int i = 0; i < 8; ++i) {
+                    const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+                    if (!present) continue;
+                    if (leaf && d->leaf_count[o.children[i]] == 1) {
+                        const octpt_sphere &x = d->spheres[d->leaf_prims[d->leaf_first[o.children[i]]]];
+                        leaf_sph[k] = make_float4(x.center[0], x.center[1], x.center[2], x.radius);
+                    }
+                    ++k;
+                }
+            }
+        }
         std::vector<float4> sph(d->sphere_count);
         std::vector<uint32_t> sph_mat(d->sphere_count);
         for (uint32_t s = 0; s < d->sphere_count; ++s) {
@@ -932,6 +951,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         DevTexture *d_texs;
         uint8_t *d_texels;
         HIP_TRY(ctx, upload(ctx, child.data(), child.size(), &d_child));
+        float4 *d_leaf_sph = nullptr;
+        if (!leaf_sph.empty()) HIP_TRY(ctx, upload(ctx, leaf_sph.data(), leaf_sph.size(), &d_leaf_sph));
         HIP_TRY(ctx, upload(ctx, d->leaf_prims, d->leaf_prim_count, &d_prims));
         HIP_TRY(ctx, upload(ctx, sph.data(), sph.size(), &d_sph));
         HIP_TRY(ctx, upload(ctx, sph_mat.data(), sph_mat.size(), &d_sph_mat));
@@ -950,6 +971,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
             HIP_TRY(ctx, upload(ctx, quads.data(), quads.size(), &d_quads));
         }
         S.node_child = d_child;
+        S.leaf_sph = d_leaf_sph;
         S.root = base[d->root];  // traversal "parent" values are child-array bases
         S.root_mask = d->octants[d->root].child_mask;
         S.node0_mask = d->octants[0].child_mask;  // base[0] == 0: a zeroed stack entry reads octant 0

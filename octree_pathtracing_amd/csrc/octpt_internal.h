@@ -80,6 +80,7 @@ struct DevScene {
     // its base; octant child = (its base, its child_mask), leaf child = (prim id, 1) or
     // (first leaf prim, prim count)
     const uint2 *node_child;
+    const float4 *leaf_sph;         // parallel to node_child: the sphere of a single-sphere leaf slot
     uint32_t root, root_mask, node0_mask, depth, n_octants;  // root = the root octant's base
     uint32_t has_cuboids;
     float octree_scale;             // 2^-depth

@@ -574,13 +574,20 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
 // rest of a multi-primitive list in a loop, keeping the closest accepted hit.
 template <int kPrims = kPrimsModels>
 __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
-                                 uint32_t &best_prim, PrimHit &best, Counters &cnt) {
+                                 uint32_t &best_prim, PrimHit &best, Counters &cnt, const float4 *pre = nullptr) {
     // three correctly-rounded divides: only scenes holding cuboids pay for them (uniform branch)
     v3 inv = V(0.0f, 0.0f, 0.0f);
     if (kPrims != kPrimsSpheres && S.has_cuboids) inv = ray_inv_dir(r.d);
     uint32_t prim = lr.x;
     if (lr.y != 1u) prim = S.leaf_prims[lr.x];
-    bool found = prim_test<kPrims>(S, r, prim, inv, t_accept, best, cnt);
+    bool found;
+    if (kPrims == kPrimsSpheres && pre && lr.y == 1u) {
+        // single-sphere leaf: its sphere arrived with the slot (leaf_sph, loaded beside node_child)
+        cnt.sph++;
+        found = sphere_test(*pre, r, prim == r.last_prim, best) && best.t <= t_accept;
+    } else {
+        found = prim_test<kPrims>(S, r, prim, inv, t_accept, best, cnt);
+    }
     if (found) best_prim = prim;
     for (uint32_t k = 1; k < lr.y; ++k) {
         const uint32_t p = S.leaf_prims[lr.x + k];
@@ -625,7 +632,11 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const bool take_leaf = live && is_leaf && E.t_min >= 0.0f && !resume;
     const bool descend = live && !is_leaf && E.t_min <= tv_max;
     uint2 slot = make_uint2(0u, 0u);
-    if (take_leaf || descend) slot = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx) - 1u))];
+    const uint32_t sidx = E.parent + __popc(E.pmask & ((1u << cidx) - 1u));
+    if (take_leaf || descend) slot = S.node_child[sidx];
+    // sphere-only scenes: a leaf's first sphere is loaded beside its slot (no dependent second load)
+    float4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (kPrims == kPrimsSpheres && take_leaf) lsph = S.leaf_sph[sidx];
     if (take_leaf) {
         // x / 2^-depth == x * 2^depth exactly (the oracle divides)
         const float cell_w = E.scale_exp2 * S.inv_octree_scale;
@@ -635,7 +646,8 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
             E.resume = true;
             return kStepLeaf;
         }
-        if (leaf_test<kPrims>(S, ray, slot, t_accept, prim, h, cnt)) return kStepHit;
+        if (leaf_test<kPrims>(S, ray, slot, t_accept, prim, h, cnt, kPrims == kPrimsSpheres ? &lsph : nullptr))
+            return kStepHit;
     }
     // Descend (:216-244) and advance (:249-260) as one select-based update: every lane computes
     // X = t_coef * f + t_corner with f = half for descend (X = t_center) and f = 0 otherwise
