@@ -991,6 +991,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.quads = d_quads;
         S.has_models = has_models ? 1u : 0u;
         S.mats = d_mats;
+        S.n_mats = d->material_count;
         S.texs = d_texs;
         S.texels = d_texels;
         S.lut_float = ctx->d_lut_float;

@@ -96,6 +96,7 @@ struct DevScene {
     const DevQuad *quads;
     uint32_t has_models;
     const DevMaterial *mats;
+    uint32_t n_mats;
     const DevTexture *texs;
     const uint8_t *texels;
     const float *lut_float;         // LUT_TABLE_FLOAT (texture.rs:51-54)

@@ -1847,10 +1847,23 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
 #ifndef OCTPT_SHADE_WAVES
 #define OCTPT_SHADE_WAVES 1
 #endif
-template <bool kNee>
-__global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene S, DevCamera C, DevRender R, WaveBuffers B,
+// scenes with at most kShadeLdsMats materials shade from an LDS copy of the table: the
+// material loads sit at the end of the dependent chain ray -> path state / primitive -> material
+#ifndef OCTPT_SHADE_LDS_MATS
+#define OCTPT_SHADE_LDS_MATS 128
+#endif
+constexpr uint32_t kShadeLdsMats = OCTPT_SHADE_LDS_MATS;
+template <bool kNee, bool kLdsMats>
+__global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items,
                                                           unsigned long long *__restrict__ stats) {
+    __shared__ DevMaterial smats[(kLdsMats && kShadeLdsMats) ? kShadeLdsMats : 1u];
+    DevScene S = Sg;
+    if constexpr (kLdsMats) {
+        for (uint32_t m = threadIdx.x; m < Sg.n_mats; m += kBlock) smats[m] = Sg.mats[m];
+        __syncthreads();
+        S.mats = smats;
+    }
     // wave w shades segment w % kSegs of queue q (grid: a multiple of kSegs waves) and appends
     // the continuing / regenerated rays to the same segment of queue q ^ 1
     const uint32_t lane = threadIdx.x & 63u;
@@ -2107,10 +2120,10 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
 
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
                            uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream) {
-    if (S.sun.sun_sampling)
-        hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
-    else
-        hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
+    const bool lds = S.n_mats <= kShadeLdsMats;
+    auto kern = S.sun.sun_sampling ? (lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
+                                   : (lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
     return hipGetLastError();
 }
 
