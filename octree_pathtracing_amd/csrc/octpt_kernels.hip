@@ -542,7 +542,7 @@ enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 // reserve registers, 7 waves/SIMD in wf_extend_kernel; kPrimsBoxes adds cuboids, kPrimsModels
 // block-model cuboids)
 template <int kPrims>
-__device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, uint32_t prim, v3 inv, float t_accept,
+__device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, uint32_t prim, float t_accept,
                                           PrimHit &h, Counters &cnt) {
     const bool self_prim = prim == r.last_prim;
     bool ok;
@@ -563,6 +563,8 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
             }
         }
         const float2 cb = S.cub_b[ci];
+        // the slab test's three correctly-rounded divides run for cuboid tests only
+        const v3 inv = ray_inv_dir(r.d);
         ok = cuboid_test(make_float4(ca.x, ca.y, ca.z, 0.0f), make_float4(ca.w, cb.x, cb.y, 0.0f), r, inv, self_prim, h);
     }
     return ok && h.t <= t_accept;
@@ -575,9 +577,6 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
 template <int kPrims = kPrimsModels>
 __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt, const float4 *pre = nullptr) {
-    // three correctly-rounded divides: only scenes holding cuboids pay for them (uniform branch)
-    v3 inv = V(0.0f, 0.0f, 0.0f);
-    if (kPrims != kPrimsSpheres && S.has_cuboids) inv = ray_inv_dir(r.d);
     uint32_t prim = lr.x;
     if (lr.y != 1u) prim = S.leaf_prims[lr.x];
     bool found;
@@ -586,13 +585,13 @@ __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr,
         cnt.sph++;
         found = sphere_test(*pre, r, prim == r.last_prim, best) && best.t <= t_accept;
     } else {
-        found = prim_test<kPrims>(S, r, prim, inv, t_accept, best, cnt);
+        found = prim_test<kPrims>(S, r, prim, t_accept, best, cnt);
     }
     if (found) best_prim = prim;
     for (uint32_t k = 1; k < lr.y; ++k) {
         const uint32_t p = S.leaf_prims[lr.x + k];
         PrimHit hk;
-        if (prim_test<kPrims>(S, r, p, inv, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
+        if (prim_test<kPrims>(S, r, p, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
             best = hk;
             best_prim = p;
             found = true;
