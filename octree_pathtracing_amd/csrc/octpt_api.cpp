@@ -993,6 +993,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.mats = d_mats;
         S.n_mats = d->material_count;
         S.texs = d_texs;
+        S.n_texs = d->texture_count;
         S.texels = d_texels;
         S.lut_float = ctx->d_lut_float;
         make_sun(d->sun, lf, S.sun);

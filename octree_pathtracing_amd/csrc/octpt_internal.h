@@ -98,6 +98,7 @@ struct DevScene {
     const DevMaterial *mats;
     uint32_t n_mats;
     const DevTexture *texs;
+    uint32_t n_texs;
     const uint8_t *texels;
     const float *lut_float;         // LUT_TABLE_FLOAT (texture.rs:51-54)
     DevSun sun;

@@ -1846,8 +1846,9 @@ __global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, Wav
 #ifndef OCTPT_SHADE_WAVES
 #define OCTPT_SHADE_WAVES 1
 #endif
-// scenes with at most kShadeLdsMats materials shade from an LDS copy of the table: the
-// material loads sit at the end of the dependent chain ray -> path state / primitive -> material
+// scenes with at most kShadeLdsMats materials and textures shade from LDS copies of the material
+// and texture tables and the sRGB LUT: these loads sit at the end of the dependent chain
+// ray -> path state / primitive -> face material -> material -> texture -> texel -> LUT
 #ifndef OCTPT_SHADE_LDS_MATS
 #define OCTPT_SHADE_LDS_MATS 128
 #endif
@@ -1856,12 +1857,20 @@ template <bool kNee, bool kLdsMats>
 __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items,
                                                           unsigned long long *__restrict__ stats) {
-    __shared__ DevMaterial smats[(kLdsMats && kShadeLdsMats) ? kShadeLdsMats : 1u];
+    constexpr uint32_t kT = (kLdsMats && kShadeLdsMats) ? kShadeLdsMats : 1u;
+    __shared__ DevMaterial smats[kT];
+    __shared__ DevTexture stexs[kT];
+    __shared__ float slut[kLdsMats ? 256 : 1];
     DevScene S = Sg;
     if constexpr (kLdsMats) {
         for (uint32_t m = threadIdx.x; m < Sg.n_mats; m += kBlock) smats[m] = Sg.mats[m];
+        for (uint32_t t = threadIdx.x; t < Sg.n_texs; t += kBlock) stexs[t] = Sg.texs[t];
+        static_assert(kBlock == 256u, "one LUT entry per thread");
+        slut[threadIdx.x] = Sg.lut_float[threadIdx.x];
         __syncthreads();
         S.mats = smats;
+        S.texs = stexs;
+        S.lut_float = slut;
     }
     // wave w shades segment w % kSegs of queue q (grid: a multiple of kSegs waves) and appends
     // the continuing / regenerated rays to the same segment of queue q ^ 1
@@ -2119,7 +2128,7 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
 
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
                            uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream) {
-    const bool lds = S.n_mats <= kShadeLdsMats;
+    const bool lds = S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats;
     auto kern = S.sun.sun_sampling ? (lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
                                    : (lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
