@@ -399,51 +399,53 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
         n = V((p.x - sp.x) / sp.w, (p.y - sp.y) / sp.w, (p.z - sp.z) / sp.w);
         mat = S.sphere_mat[prim];
         uv_ready = false;  // sphere uv only feeds image textures (computed lazily below)
-    } else if (S.has_models && S.cub_model[prim & ~kPrimCuboidBit] != OCTPT_MODEL_NONE) {
-        // block-model hit [C19]: the hit record holds the instance and t; the quad is the one
-        // model_test chose, found again by the same computation with t_next = t
-        const uint32_t ci = prim & ~kPrimCuboidBit;
-        const float4 ca = S.cub_a[ci];
-        uint32_t q = 0u;
-        float al = 0.0f, be = 0.0f, tq;
-        TraceRay tr;
-        tr.o = r.o;
-        tr.d = r.d;
-        tr.last_prim = r.last_prim;
-        tr.self_inward = false;
-        model_test(S, tr, V(ca.x, ca.y, ca.z), S.cub_model[ci], h.t, tq, q, al, be);
-        const DevQuad &Q = S.quads[q];
-        n = V(Q.n_tv0.x, Q.n_tv0.y, Q.n_tv0.z);
-        mat = __float_as_uint(Q.u_mat.w);
-        const float tu0 = Q.v_tu0.w, tu1 = Q.w_tu1.w, tv0 = Q.n_tv0.w, tv1 = Q.tv1.x;
-        u = tu0 + al * (tu1 - tu0);  // quad.rs:194-197
-        v = tv0 + be * (tv1 - tv0);
-        uv_ready = true;
-        prim = kQuadKey | q;  // the self-intersection key of the next segment
     } else {
+        // the box, its face material (the face is in the hit record) and its model id load together
         const uint32_t ci = prim & ~kPrimCuboidBit;
         const float4 ca = S.cub_a[ci];
         const float2 cb = S.cub_b[ci];
-        const float4 bmin = make_float4(ca.x, ca.y, ca.z, 0.0f), bmax = make_float4(ca.w, cb.x, cb.y, 0.0f);
-        n = V(0.0f, 0.0f, 0.0f);
         const uint32_t axis = h.axis();
         const float nsgn = h.nsgn();
-        if (axis == 0u) n.x = nsgn; else if (axis == 1u) n.y = nsgn; else n.z = nsgn;
-        const float ex = bmax.x - bmin.x, ey = bmax.y - bmin.y, ez = bmax.z - bmin.z;
-        if (axis == 0u) {
-            u = (p.z - bmin.z) / ez; v = (p.y - bmin.y) / ey;
-            if (r.d.x < 0.0f) u = 1.0f - u;
-        } else if (axis == 1u) {
-            u = (p.x - bmin.x) / ex; v = (p.z - bmin.z) / ez;
-            if (r.d.y < 0.0f) v = 1.0f - v;
-        } else {
-            u = (p.x - bmin.x) / ex; v = (p.y - bmin.y) / ey;
-            if (r.d.z < 0.0f) u = 1.0f - u;
-        }
-        u = fabsf(u);
-        v = fabsf(v);
         mat = S.cub_mat[6u * ci + face_index(axis, nsgn)];
-        uv_ready = true;
+        const uint32_t mdl = S.has_models ? S.cub_model[ci] : OCTPT_MODEL_NONE;
+        if (mdl != OCTPT_MODEL_NONE) {
+            // block-model hit [C19]: the hit record holds the instance and t; the quad is the one
+            // model_test chose, found again by the same computation with t_next = t
+            uint32_t q = 0u;
+            float al = 0.0f, be = 0.0f, tq;
+            TraceRay tr;
+            tr.o = r.o;
+            tr.d = r.d;
+            tr.last_prim = r.last_prim;
+            tr.self_inward = false;
+            model_test(S, tr, V(ca.x, ca.y, ca.z), mdl, h.t, tq, q, al, be);
+            const DevQuad &Q = S.quads[q];
+            n = V(Q.n_tv0.x, Q.n_tv0.y, Q.n_tv0.z);
+            mat = __float_as_uint(Q.u_mat.w);
+            const float tu0 = Q.v_tu0.w, tu1 = Q.w_tu1.w, tv0 = Q.n_tv0.w, tv1 = Q.tv1.x;
+            u = tu0 + al * (tu1 - tu0);  // quad.rs:194-197
+            v = tv0 + be * (tv1 - tv0);
+            uv_ready = true;
+            prim = kQuadKey | q;  // the self-intersection key of the next segment
+        } else {
+            const float4 bmin = make_float4(ca.x, ca.y, ca.z, 0.0f), bmax = make_float4(ca.w, cb.x, cb.y, 0.0f);
+            n = V(0.0f, 0.0f, 0.0f);
+            if (axis == 0u) n.x = nsgn; else if (axis == 1u) n.y = nsgn; else n.z = nsgn;
+            const float ex = bmax.x - bmin.x, ey = bmax.y - bmin.y, ez = bmax.z - bmin.z;
+            if (axis == 0u) {
+                u = (p.z - bmin.z) / ez; v = (p.y - bmin.y) / ey;
+                if (r.d.x < 0.0f) u = 1.0f - u;
+            } else if (axis == 1u) {
+                u = (p.x - bmin.x) / ex; v = (p.z - bmin.z) / ez;
+                if (r.d.y < 0.0f) v = 1.0f - v;
+            } else {
+                u = (p.x - bmin.x) / ex; v = (p.y - bmin.y) / ey;
+                if (r.d.z < 0.0f) u = 1.0f - u;
+            }
+            u = fabsf(u);
+            v = fabsf(v);
+            uv_ready = true;
+        }
     }
     r.o = p;
     r.n = n;
