@@ -1448,6 +1448,9 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #ifndef OCTPT_EXTEND_WAVES
 #define OCTPT_EXTEND_WAVES 1
 #endif
+#ifndef OCTPT_EXTEND_NESTED
+#define OCTPT_EXTEND_NESTED 1
+#endif
 template <bool kDefer, int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            uint32_t leaf_batch, unsigned long long *__restrict__ stats) {
@@ -1501,6 +1504,35 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
                 }
             }
         }
+#if OCTPT_EXTEND_NESTED
+        if constexpr (!kDefer) {
+            // inner loop: step until `refill` lanes are idle (every lane, once no ray is left); its
+            // only per-iteration bookkeeping is one ballot, a popcount and a scalar branch
+            const uint32_t stop_at = rays_left ? refill : 64u;
+            if ((uint32_t)__popcll(__ballot(!active)) < stop_at) do {
+#ifdef OCTPT_INJECT_SALU
+                {
+                    uint32_t sd = __builtin_amdgcn_readfirstlane(pos);
+#pragma unroll
+                    for (int k = 0; k < OCTPT_INJECT_SALU; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sd));
+                    if (sd == 0xDEADBEEFu) segs_w++;
+                }
+#endif
+                if (active) {
+                    uint32_t prim = kPrimNone;
+                    PrimHit h;
+                    const int rs = esvo_step<false, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
+                    if (rs != kStepContinue) {
+                        B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                        cnt.steps += E.iter;
+                        active = false;
+                    }
+                }
+            } while ((uint32_t)__popcll(__ballot(!active)) < stop_at);  // at the bottom: no phi copies
+            more = rays_left;  // wave-uniform; every lane is idle when it is false
+            continue;
+        }
+#endif
         const uint64_t am = __ballot(active);
         // the loop ends after a pass in which no lane was active and no ray was left (with am == 0
         // the step below does nothing).  Testing it at the bottom, made uniform by readfirstlane,
