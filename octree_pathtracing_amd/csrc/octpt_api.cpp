@@ -30,7 +30,7 @@ constexpr uint64_t kMaxChunkPaths = 1ull << 30;    // colour buffer: up to 16 Gi
 constexpr uint32_t kLookahead = 3;                  // host steering: iterations queued ahead of the check
 constexpr uint32_t kDefaultPool = 256u << 20;        // path slots in flight (28.7 GB of queues + path state)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
-constexpr uint32_t kDefaultRefill = 16;              // extend: idle lanes before a wave refills
+constexpr uint32_t kDefaultRefill = 0;               // extend: idle lanes before a wave refills (0: adaptive)
 constexpr uint32_t kDefaultLeafBatch = 0;            // extend: parked lanes before a wave tests leaves (0: inline)
 
 uint32_t env_u32(const char *name, uint32_t dflt) {
@@ -762,7 +762,11 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->num_cu = prop.multiProcessorCount;
     ctx->pool_cap = env_u32("OCTPT_POOL", kDefaultPool);
     ctx->chunk_cap = std::min<uint64_t>(env_u32("OCTPT_CHUNK", (uint32_t)kMaxChunkPaths), kMaxChunkPaths);
-    ctx->refill = std::max<uint32_t>(std::min<uint32_t>(env_u32("OCTPT_REFILL", kDefaultRefill), 64u), 1u);
+    // OCTPT_REFILL=n fixes the threshold (clamped to [1, 64]); unset: adaptive per wave (0)
+    const char *refill_env = std::getenv("OCTPT_REFILL");
+    ctx->refill = (refill_env && *refill_env)
+                      ? std::max<uint32_t>(std::min<uint32_t>(env_u32("OCTPT_REFILL", 16u), 64u), 1u)
+                      : kDefaultRefill;
     ctx->leaf_batch = std::min<uint32_t>(env_u32("OCTPT_LEAF_BATCH", kDefaultLeafBatch), 64u);
     if (const char *m = std::getenv("OCTPT_EXTEND")) {  // extend variant: "split" = wave-specialised
         if (std::string(m) == "split") ctx->leaf_batch = kLeafSplit;

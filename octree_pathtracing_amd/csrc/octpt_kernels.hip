@@ -1443,14 +1443,19 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 }
 
 // extend: closest-hit queries for every queued ray.  Persistent waves; a lane that finishes
-// its ray idles until at least `refill` lanes of the wave are idle, then the wave pulls that
-// many rays from the queue with one atomic (Aila & Laine dynamic fetch).
+// its ray idles until at least `refill` lanes of the wave are idle, then the wave hands the idle
+// lanes the next positions of the chunk it has claimed (Aila & Laine dynamic fetch, with the
+// atomic of the next claim already in flight).
 #ifndef OCTPT_EXTEND_WAVES
 #define OCTPT_EXTEND_WAVES 1
 #endif
 #ifndef OCTPT_EXTEND_NESTED
 #define OCTPT_EXTEND_NESTED 1
 #endif
+// positions a wave claims from its segment at a time (one atomic per claim)
+constexpr uint32_t kClaim = 64u;
+// refill == 0 (adaptive): rays shorter than this many ESVO steps on average refill 32 at a time
+constexpr uint32_t kShortRaySteps = 56u;
 template <bool kDefer, int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            uint32_t leaf_batch, unsigned long long *__restrict__ stats) {
@@ -1474,41 +1479,66 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
     uint2 leaf = make_uint2(0u, 0u);
     float t_accept = 0.0f;
     bool more = true;
+    // chunked claims: the wave owns [c_next, c_end) of segment seg and holds one further claim in
+    // flight (lane 0's atomic result, read only when the owned chunk runs out), so a refill hands
+    // out positions without waiting on an atomic's round trip
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t c_next = 0u, c_end = 0u, claim_v = 0u;
+    uint32_t thr = refill ? refill : 16u;  // idle lanes that trigger a refill (wave-uniform)
+    uint32_t lane_rays = 0u;                // rays this lane started (adaptive threshold)
+    if (lane == 0u)
+        claim_v = __hip_atomic_fetch_add(B.ctrl + ctr_head(q, seg), kClaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     do {
-        // refill (refill >= 1, clamped by the host): one scalar test per iteration
+        // refill: one scalar test per iteration
         const bool idle = !active;
         const uint64_t im = __ballot(idle);
-        if (rays_left && (uint32_t)__popcll(im) >= refill) {
-            const uint32_t my = wave_ticket(B.ctrl + ctr_head(q, seg), idle);
-            bool dry = false;
+        if (rays_left && (uint32_t)__popcll(im) >= thr) {
+            if (c_next >= c_end) {  // the owned chunk ran out: take the claim in flight
+                c_next = __builtin_amdgcn_readfirstlane(claim_v);
+                c_end = c_next < seg_n ? __builtin_amdgcn_readfirstlane(min(c_next + kClaim, seg_n))
+                                       : c_next;
+                if (c_next >= c_end) {
+                    // segment drained: lane j checks segment j, the wave moves on and claims there
+                    const uint32_t j = lane;
+                    const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, j)) < B.ctrl[ctr_count(q, j)]);
+                    rays_left = m != 0ull;
+                    if (rays_left) {
+                        seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
+                        seg_n = B.ctrl[ctr_count(q, seg)];
+                    }
+                }
+                if (rays_left && lane == 0u)
+                    claim_v = __hip_atomic_fetch_add(B.ctrl + ctr_head(q, seg), kClaim,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const uint32_t avail = c_end - c_next;
             if (idle) {
-                if (my < seg_n) {
-                    pos = seg * B.seg_cap + my;
+                const uint32_t r = lanes_below(im);
+                if (r < avail) {
+                    pos = seg * B.seg_cap + c_next + r;
                     const float4 r0 = ray0[pos], r1 = ray1[pos];
                     tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk);
                     active = true;
-                } else {
-                    dry = true;
+                    lane_rays++;
                 }
             }
-            segs_w += (uint32_t)__popcll(__ballot(idle && !dry));  // uniform point: a scalar counter
-            if (__ballot(dry) != 0ull) {  // segment drained: lane j checks segment j, the wave moves on
-                const uint32_t j = threadIdx.x & 63u;
-                const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, j)) < B.ctrl[ctr_count(q, j)]);
-                rays_left = m != 0ull;
-                if (rays_left) {
-                    seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
-                    seg_n = B.ctrl[ctr_count(q, seg)];
-                }
+            const uint32_t took = min((uint32_t)__popcll(im), avail);
+            segs_w += took;
+            c_next += took;
+            if (refill == 0u) {
+                // adaptive threshold: when most lanes' rays so far averaged fewer
+                // than kShortRaySteps ESVO steps, the wave refills 32 at a time, else 16
+                const bool short_rays = cnt.steps < kShortRaySteps * lane_rays;
+                thr = __popcll(__ballot(short_rays)) > 32 ? 32u : 16u;
             }
         }
 #if OCTPT_EXTEND_NESTED
         if constexpr (!kDefer) {
             // inner loop: step until `refill` lanes are idle (every lane, once no ray is left); its
             // only per-iteration bookkeeping is one ballot, a popcount and a scalar branch
-            const uint32_t stop_at = rays_left ? refill : 64u;
+            const uint32_t stop_at = rays_left ? thr : 64u;
             if ((uint32_t)__popcll(__ballot(!active)) < stop_at) do {
 #ifdef OCTPT_INJECT_SALU
                 {
@@ -2152,7 +2182,9 @@ hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuff
 
 hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill,
                             uint32_t leaf_batch, int grid, unsigned long long *stats, hipStream_t stream) {
-    // leaf_batch 0: test leaves inside the step (no deferral)
+    // leaf_batch 0: test leaves inside the step (no deferral).  refill 0 (adaptive) is
+    // wf_extend_kernel's; the experimental kernels take 16 for it
+    if (refill == 0u && ((leaf_batch & kLeafSpec) || leaf_batch == kLeafSplit)) refill = 16u;
     void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &leaf_batch, &stats};
     const hipError_t e = hipLaunchKernel(extend_instance(S, leaf_batch), dim3(grid), dim3(kBlock), args,
                                          extend_lds_bytes(S, leaf_batch), stream);
