@@ -1538,7 +1538,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(D
         if constexpr (!kDefer) {
             // inner loop: step until `refill` lanes are idle (every lane, once no ray is left); its
             // only per-iteration bookkeeping is one ballot, a popcount and a scalar branch
-            const uint32_t stop_at = rays_left ? thr : 64u;
+            const uint32_t stop_at = __builtin_amdgcn_readfirstlane(rays_left ? thr : 64u);  // keeps the loop scalar
             if ((uint32_t)__popcll(__ballot(!active)) < stop_at) do {
 #ifdef OCTPT_INJECT_SALU
                 {
