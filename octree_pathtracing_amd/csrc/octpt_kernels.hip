@@ -682,10 +682,11 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     E.idx = descend ? step_mask : (E.idx ^ step_mask);
     bool escaped = false;
     if (!descend && (E.idx & step_mask) != 0u) {  // pop (:262-299)
-        uint32_t diff = 0u;
-        if (step_mask & 1u) diff |= __float_as_uint(E.pos.x) ^ __float_as_uint(E.pos.x + E.scale_exp2);
-        if (step_mask & 2u) diff |= __float_as_uint(E.pos.y) ^ __float_as_uint(E.pos.y + E.scale_exp2);
-        if (step_mask & 4u) diff |= __float_as_uint(E.pos.z) ^ __float_as_uint(E.pos.z + E.scale_exp2);
+        // the three axes' differing bits are selected, not branched on (no exec-mask region)
+        const uint32_t dx = __float_as_uint(E.pos.x) ^ __float_as_uint(E.pos.x + E.scale_exp2);
+        const uint32_t dy = __float_as_uint(E.pos.y) ^ __float_as_uint(E.pos.y + E.scale_exp2);
+        const uint32_t dz = __float_as_uint(E.pos.z) ^ __float_as_uint(E.pos.z + E.scale_exp2);
+        const uint32_t diff = ((step_mask & 1u) ? dx : 0u) | ((step_mask & 2u) ? dy : 0u) | ((step_mask & 4u) ? dz : 0u);
         const uint32_t scale_raw = diff ? 31u - (uint32_t)__clz(diff) : 0xFFFFFFFFu;
         // escaping the root is a miss (:281-283); its lane finishes the block on a clamped scale
         // and reports the miss at the end, so the pop stays one branch level

@@ -357,6 +357,35 @@ def test_wavefront_small_pool_many_chunks(torch_cuda, renderer):
     assert np.array_equal(ref[0], out[0]) and np.array_equal(ref[1], out[1])
 
 
+@pytest.mark.parametrize("config", ["C2", "C5"])
+def test_refill_schedules_identical(torch_cuda, renderer, config):
+    """The extend schedule is invisible in the results: fixed refill thresholds 1 / 7 / 32 / 64 and the
+    adaptive default, with a pool small enough that waves cross many 64-ray claim
+    chunks and drain segments, give the same radiance, per-pixel segment counts and statistics."""
+    import os
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    sc, cam, rs = S.make_config(config)
+    rs.width, rs.height, rs.spp = 96, 40, 2
+    ref = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    for refill in ("1", "7", "32", "64", ""):
+        os.environ["OCTPT_POOL"] = "3000"
+        if refill:
+            os.environ["OCTPT_REFILL"] = refill
+        try:
+            r = HipRenderer(0)
+            out = gpu_render(torch_cuda, r, sc, cam, rs)
+            r.close()
+        finally:
+            os.environ.pop("OCTPT_POOL", None)
+            os.environ.pop("OCTPT_REFILL", None)
+        assert np.array_equal(ref[0], out[0]), refill
+        assert np.array_equal(ref[1], out[1]), refill
+        for k in ("paths", "segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events"):
+            assert ref[2][k] == out[2][k], (refill, k)
+
+
 GOLDEN = __import__("pathlib").Path(__file__).resolve().parent / "golden"
 
 
