@@ -536,6 +536,9 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
+#ifndef OCTPT_HIT_FALLTHROUGH
+#define OCTPT_HIT_FALLTHROUGH 1
+#endif
 
 
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
@@ -638,6 +641,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // sphere-only scenes: a leaf's first sphere is loaded beside its slot (no dependent second load)
     float4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (kPrims == kPrimsSpheres && take_leaf) lsph = S.leaf_sph[sidx];
+    bool leaf_hit = false;
     if (take_leaf) {
         // x / 2^-depth == x * 2^depth exactly (the oracle divides)
         const float cell_w = E.scale_exp2 * S.inv_octree_scale;
@@ -647,8 +651,14 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
             E.resume = true;
             return kStepLeaf;
         }
+#if OCTPT_HIT_FALLTHROUGH
+        // a hit lane runs the advance below too (its state is discarded): the descend / advance
+        // block then needs no exec-mask region of its own
+        leaf_hit = leaf_test<kPrims>(S, ray, slot, t_accept, prim, h, cnt, kPrims == kPrimsSpheres ? &lsph : nullptr);
+#else
         if (leaf_test<kPrims>(S, ray, slot, t_accept, prim, h, cnt, kPrims == kPrimsSpheres ? &lsph : nullptr))
             return kStepHit;
+#endif
     }
     // Descend (:216-244) and advance (:249-260) as one select-based update: every lane computes
     // X = t_coef * f + t_corner with f = half for descend (X = t_center) and f = 0 otherwise
@@ -709,7 +719,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         E.idx = (shx & 1u) | ((shy & 1u) << 1) | ((shz & 1u) << 2);
         E.h = 0.0f;
     }
-    return escaped ? kStepMiss : kStepContinue;
+    return leaf_hit ? kStepHit : (escaped ? kStepMiss : kStepContinue);
 }
 
 // ---------------------------------------------------------------------------
