@@ -1463,12 +1463,26 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #ifndef OCTPT_EXTEND_NESTED
 #define OCTPT_EXTEND_NESTED 1
 #endif
+// minimum waves per SIMD a wf_extend_kernel instance is compiled for (register budget)
+// (measured at 64 spp against the unconstrained allocation: the few spilled dwords sit in cold
+// code, the extra waves hide the slot loads' latency)
+#ifndef OCTPT_SPH_WAVES
+#define OCTPT_SPH_WAVES 8  // 71 -> 64 VGPRs, 20 B/lane spilled: C3 +2.0 %
+#endif
+#ifndef OCTPT_BOX_WAVES
+#define OCTPT_BOX_WAVES 7  // 78 -> 72 VGPRs, 20 B/lane spilled: C4 +5.5 % (8 waves: -5 %)
+#endif
+#ifndef OCTPT_MDL_WAVES
+#define OCTPT_MDL_WAVES 6  // 95 -> 80 VGPRs, 36 B/lane spilled: C5 +5.4 %
+#endif
+#define OCTPT_EXTEND_WAVES_OF(k) \
+    ((k) == kPrimsSpheres ? OCTPT_SPH_WAVES : (k) == kPrimsBoxes ? OCTPT_BOX_WAVES : OCTPT_MDL_WAVES)
 // positions a wave claims from its segment at a time (one atomic per claim)
 constexpr uint32_t kClaim = 64u;
 // refill == 0 (adaptive): rays shorter than this many ESVO steps on average refill 32 at a time
 constexpr uint32_t kShortRaySteps = 56u;
 template <bool kDefer, int kPrims>
-__global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
+__global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            uint32_t leaf_batch, unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
     const Stack stk = stack_of(lds_stack, S.depth);
