@@ -552,7 +552,8 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
                      ctx->num_cu, ctx->S.depth, ctx->S.has_cuboids, ctx->leaf_batch, pool);
     // shade maps waves to queue segments: a multiple of kSegs waves (kSegs / 4 blocks)
     const int seg_blocks = (int)(kSegs * 64u / kBlock);
-    const int grid_shade = (ctx->num_cu * 4 + seg_blocks - 1) / seg_blocks * seg_blocks;
+    const int shade_bpc = (int)std::min<uint32_t>(env_u32("OCTPT_SHADE_BPC", 4u), 8u);  // blocks per CU
+    const int grid_shade = (ctx->num_cu * shade_bpc + seg_blocks - 1) / seg_blocks * seg_blocks;
     const WaveBuffers &B = ctx->wb;
     for (uint32_t c0 = 0, c1 = 0; c0 < R.spp_count; c0 = c1) {
         c1 = c0 + std::min(chunk_spp, R.spp_count - c0);
