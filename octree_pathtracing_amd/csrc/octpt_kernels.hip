@@ -536,6 +536,9 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
+#ifndef OCTPT_FLAT_EXIT
+#define OCTPT_FLAT_EXIT 1
+#endif
 #ifndef OCTPT_HIT_FALLTHROUGH
 #define OCTPT_HIT_FALLTHROUGH 1
 #endif
@@ -616,7 +619,13 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
                                 uint32_t &prim, PrimHit &h, uint2 &leaf, float &t_accept) {
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
     const bool resume = kDefer && E.resume;
-    if (!resume) {
+    bool stopped = false;  // OCTPT_FLAT_EXIT: the step-limit / max_dst miss, taken at the end
+    if (!kDefer && OCTPT_FLAT_EXIT) {
+        // the lane runs the step with no memory side effects (not live) and reports the miss at
+        // the end, so the exit costs no exec-mask region
+        stopped = E.iter >= OCTREE_MAX_STEPS || (max_dst >= 0.0f && E.t_min > max_dst);
+        E.iter += stopped ? 0u : 1u;
+    } else if (!resume) {
         // on a resumed step these were checked before the deferred leaf: iter may now equal
         // OCTREE_MAX_STEPS, and exiting here is the same miss the reference reaches after its advance
         if (E.iter >= OCTREE_MAX_STEPS) return kStepMiss;
@@ -631,7 +640,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const bool is_leaf = (E.pmask >> (cidx + 8u)) & 1u;
     // :142-244.  Leaf (t_min >= 0) and descend (t_min <= min(t_max, tc_max)) lanes share one slot
     // load instruction: on CDNA4 a scattered load costs the vector-memory pipe per instruction.
-    const bool live = present && E.t_min <= E.t_max;
+    const bool live = present && E.t_min <= E.t_max && !stopped;
     const float tv_max = tmn(E.t_max, tc_max);
     const bool take_leaf = live && is_leaf && E.t_min >= 0.0f && !resume;
     const bool descend = live && !is_leaf && E.t_min <= tv_max;
@@ -719,7 +728,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         E.idx = (shx & 1u) | ((shy & 1u) << 1) | ((shz & 1u) << 2);
         E.h = 0.0f;
     }
-    return leaf_hit ? kStepHit : (escaped ? kStepMiss : kStepContinue);
+    return leaf_hit ? kStepHit : ((escaped || stopped) ? kStepMiss : kStepContinue);
 }
 
 // ---------------------------------------------------------------------------
