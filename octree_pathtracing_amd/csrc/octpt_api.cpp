@@ -29,7 +29,7 @@ constexpr uint64_t kMaxChunkPaths = 1ull << 31;    // colour buffer: up to 32 Gi
 constexpr uint64_t kDefaultChunkPaths = 1ull << 29;  // 4K: 64-spp chunks (C5 4634 vs 3882 Mrays/s at 2^30; C3 stays one chunk)
                                                     // (C3 = 530 M paths = one chunk: one drain tail)
 constexpr uint32_t kLookahead = 3;                  // host steering: iterations queued ahead of the check
-constexpr uint32_t kDefaultPool = 256u << 20;        // path slots in flight (28.7 GB of queues + path state)
+constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (57 GB of queues + path state)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
 constexpr uint32_t kDefaultRefill = 0;               // extend: idle lanes before a wave refills (0: adaptive)
 constexpr uint32_t kDefaultLeafBatch = 0;            // extend: parked lanes before a wave tests leaves (0: inline)
