@@ -1241,8 +1241,14 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
 // material 0 or Sun::flat_shading (scene/mod.rs:447-452).  Coherent primary rays: one thread per
 // pixel in 8x8 tiles (one tile per wave), no queues.
 // ===========================================================================
+#ifndef OCTPT_PREVIEW_BOUNDS
+#define OCTPT_PREVIEW_BOUNDS 1
+#endif
+// one wave per SIMD above the natural allocation (78 / 86 / 102 VGPRs -> 72 / 80 / 96), as for extend
+#define OCTPT_PREVIEW_WAVES_OF(k) \
+    (OCTPT_PREVIEW_BOUNDS ? ((k) == kPrimsSpheres ? 7 : (k) == kPrimsBoxes ? 6 : 5) : 1)
 template <int kPrims>
-__global__ __launch_bounds__(kBlock) void preview_kernel(DevScene S, DevCamera C, DevRender R,
+__global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void preview_kernel(DevScene S, DevCamera C, DevRender R,
                                                          float4 *__restrict__ accum, uint32_t *__restrict__ segcount,
                                                          unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
