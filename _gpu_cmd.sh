@@ -1,7 +1,7 @@
 set -e
-mkdir -p gpurun_out/pvb
-OCTPT_LIB=build_variants/pvb/liboctpt.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "preview" --timeout 300 --timeout-method thread > gpurun_out/pvb/pytest.log 2>&1 || { tail -40 gpurun_out/pvb/pytest.log; exit 1; }
-tail -1 gpurun_out/pvb/pytest.log
-for c in C3 C4 C5; do for v in cur pvb cur pvb; do
-echo "$c $v $(OCTPT_LIB=build_variants/$v/liboctpt.so timeout -k 10 200 python -u scripts/spp_sweep.py $c 1 1 1 1 --preview 2>/dev/null | tail -1)"
-done; done
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/final_pytest.log 2>&1 || { tail -40 gpurun_out/final_pytest.log; exit 1; }
+tail -1 gpurun_out/final_pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/final_smoke.log 2>&1 || { tail -20 gpurun_out/final_smoke.log; exit 1; }
+tail -1 gpurun_out/final_smoke.log
+timeout -k 10 300 python -u bench.py > gpurun_out/final_bench.json 2> gpurun_out/final_bench.err || { tail -20 gpurun_out/final_bench.err; exit 1; }
+tail -1 gpurun_out/final_bench.json | cut -c90-200
