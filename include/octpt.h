@@ -43,10 +43,15 @@ typedef struct octpt_frame octpt_frame;
 typedef struct octpt_octree octpt_octree;
 
 /* new_octree::Octant (src/octree/new_octree.rs:70-74) in C layout, 36 bytes.
- * child_mask bit i = child i present, bit i+8 = child i is a leaf (the
- * OctantChildIterator reading, new_octree.rs:84-100).  children[i] is an octant
- * index (present, not leaf) or the leaf payload (present + leaf).  Child index
- * i = x | y << 1 | z << 2 (the ESVO/Morton child order, octree_traversal.rs:22-24). */
+ * Two mask bits per child i, (bit i, bit i+8):
+ *   (0,0) empty; (1,1) leaf, children[i] = the leaf payload (leaf table index);
+ *   (1,0) octant, children[i] = octant index -- the OctantChildIterator reading
+ *         (new_octree.rs:84-100), what octpt_build_octree writes;
+ *   (0,1) octant, children[i] = octant index -- the form Octant::set_mask_for writes for
+ *         ChildType::Octant (new_octree.rs:160-178), i.e. every tree the reference's
+ *         expand_by / RegionOctreeBuilder / SectionOctantBuilder build.
+ * Leaves may sit at any level (LOD leaves above the bottom, new_octree.rs:534-536).
+ * Child index i = x | y << 1 | z << 2 (the ESVO/Morton child order, octree_traversal.rs:22-24). */
 typedef struct octpt_octant {
     uint16_t child_mask;
     uint16_t reserved;

@@ -19,6 +19,7 @@
 
 #include "../../include/octpt.h"
 #include "octpt_internal.h"
+#include "octpt_mask.h"
 
 using namespace octpt;
 
@@ -228,18 +229,20 @@ hipError_t upload(octpt_ctx *ctx, const T *src, size_t n, T **dst) {
     return hipSuccess;
 }
 
-// memoised subtree height with cycle detection; returns -1 on a cycle or bad index
-int subtree_height(const octpt_scene_desc &d, uint32_t node, std::vector<int8_t> &h, int level) {
+// memoised subtree height with cycle detection; returns -1 on a cycle or bad index.
+// masks: the octants' child masks in the reader form (normalized_mask, C21)
+int subtree_height(const octpt_scene_desc &d, const std::vector<uint16_t> &masks, uint32_t node, std::vector<int8_t> &h,
+                   int level) {
     if (level > (int)kMaxDepth + 1) return -1;
     if (h[node] == -2) return -1;  // on the current DFS path: cycle
     if (h[node] >= 0) return h[node];
     h[node] = -2;
     int best = 1;
-    const octpt_octant &o = d.octants[node];
+    const uint32_t m = masks[node];
     for (int i = 0; i < 8; ++i) {
-        const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+        const bool present = (m >> i) & 1, leaf = (m >> (i + 8)) & 1;
         if (!present || leaf) continue;
-        const int ch = subtree_height(d, o.children[i], h, level + 1);
+        const int ch = subtree_height(d, masks, d.octants[node].children[i], h, level + 1);
         if (ch < 0) return -1;
         best = std::max(best, ch + 1);
     }
@@ -269,7 +272,8 @@ DevQuad make_dev_quad(const octpt_quad &x) {
     return q;
 }
 
-octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d) {
+// masks (out): every octant's child mask in the reader form (C21)
+octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d, std::vector<uint16_t> &masks) {
     if (!d) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene is NULL");
     if (d->abi_version != OCTPT_ABI_VERSION) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene abi_version mismatch");
     if (d->depth < 1 || d->depth > kMaxDepth) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree depth must be in [1, 21]");
@@ -284,19 +288,26 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d) {
         return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^27 - 1 spheres or cuboids");
     if (d->sphere_count && !d->spheres) return fail(ctx, OCTPT_ERR_INVALID_ARG, "spheres is NULL");
     if (d->cuboid_count && !d->cuboids) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboids is NULL");
+    // both octant encodings are accepted (C21): (present, leaf bit) = (1,0) or set_mask_for's (0,1)
+    masks.resize(d->octant_count);
     for (uint32_t n = 0; n < d->octant_count; ++n) {
         const octpt_octant &o = d->octants[n];
+        const uint32_t m = masks[n] = normalized_mask(o.child_mask);
         for (int i = 0; i < 8; ++i) {
-            const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+            const bool present = (m >> i) & 1, leaf = (m >> (i + 8)) & 1;
             if (!present) continue;
             if (leaf && o.children[i] >= d->leaf_table_size)
-                return fail(ctx, OCTPT_ERR_INVALID_ARG, "leaf payload " + std::to_string(o.children[i]) + " out of range");
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "octant " + std::to_string(n) + " child " + std::to_string(i) +
+                                                            ": leaf payload " + std::to_string(o.children[i]) +
+                                                            " out of range");
             if (!leaf && o.children[i] >= d->octant_count)
-                return fail(ctx, OCTPT_ERR_INVALID_ARG, "child octant index out of range");
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "octant " + std::to_string(n) + " child " + std::to_string(i) +
+                                                            ": child octant index " + std::to_string(o.children[i]) +
+                                                            " out of range");
         }
     }
     std::vector<int8_t> h(d->octant_count, -1);
-    const int height = subtree_height(*d, d->root, h, 0);
+    const int height = subtree_height(*d, masks, d->root, h, 0);
     if (height < 0) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree contains a cycle");
     if ((uint32_t)height > d->depth) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree is deeper than its declared depth");
     for (uint32_t l = 0; l < d->leaf_table_size; ++l)
@@ -829,7 +840,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
     join_inflight(ctx);
     try {
-        octpt_status st = validate_scene(ctx, d);
+        std::vector<uint16_t> masks;  // reader-form child masks (C21)
+        octpt_status st = validate_scene(ctx, d, masks);
         if (st != OCTPT_OK) return st;
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -842,7 +854,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         size_t n_slots = 0;
         for (uint32_t n = 0; n < d->octant_count; ++n) {
             base[n] = (uint32_t)n_slots;
-            n_slots += (size_t)__builtin_popcount(d->octants[n].child_mask & 0xFFu);
+            n_slots += (size_t)__builtin_popcount(masks[n] & 0xFFu);
         }
         if (n_slots >= 0xFFFFFFFFull) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree too large");
         // + 8 zero slots: a child index computed for an absent child of the last octant stays in bounds
@@ -851,11 +863,11 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
             const octpt_octant &o = d->octants[n];
             uint32_t k = base[n];
             for (int i = 0; i < 8; ++i) {
-                const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+                const bool present = (masks[n] >> i) & 1, leaf = (masks[n] >> (i + 8)) & 1;
                 if (!present) continue;
                 const uint32_t v = o.children[i];
                 if (!leaf) {
-                    child[k++] = make_uint2(base[v], d->octants[v].child_mask);
+                    child[k++] = make_uint2(base[v], masks[v]);
                 } else if (d->leaf_count[v] == 1) {  // single-primitive leaf: the prim id itself
                     child[k++] = make_uint2(d->leaf_prims[d->leaf_first[v]], 1u);
                 } else {
@@ -872,7 +884,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
                 const octpt_octant &o = d->octants[n];
                 uint32_t k = base[n];
                 for (int i = 0; i < 8; ++i) {
-                    const bool present = (o.child_mask >> i) & 1, leaf = (o.child_mask >> (i + 8)) & 1;
+                    const bool present = (masks[n] >> i) & 1, leaf = (masks[n] >> (i + 8)) & 1;
                     if (!present) continue;
                     if (leaf && d->leaf_count[o.children[i]] == 1) {
                         const octpt_sphere &x = d->spheres[d->leaf_prims[d->leaf_first[o.children[i]]]];
@@ -979,8 +991,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.node_child = d_child;
         S.leaf_sph = d_leaf_sph;
         S.root = base[d->root];  // traversal "parent" values are child-array bases
-        S.root_mask = d->octants[d->root].child_mask;
-        S.node0_mask = d->octants[0].child_mask;  // base[0] == 0: a zeroed stack entry reads octant 0
+        S.root_mask = masks[d->root];
+        S.node0_mask = masks[0];  // base[0] == 0: a zeroed stack entry reads octant 0
         S.depth = d->depth;
         S.n_octants = d->octant_count;
         S.has_cuboids = d->cuboid_count ? 1u : 0u;

@@ -12,6 +12,7 @@
 #include <cstring>
 
 #include "../../include/octpt.h"
+#include "octpt_mask.h"
 
 namespace {
 constexpr uint32_t kMaxScale = 23u;   // OCTREE_MAX_SCALE, octree_traversal.rs:14
@@ -74,7 +75,7 @@ extern "C" octpt_status octpt_traversal_data(const octpt_octant *octants, uint32
         for (int i = 0; i < 3; ++i) t_corner[i] = pos[i] * t_coef[i] - t_bias[i];
         const float tc_max = mn(mn(t_corner[0], t_corner[1]), t_corner[2]);
         const uint32_t cidx = idx ^ mirror;
-        const uint32_t mask = octants[parent].child_mask;
+        const uint32_t mask = octpt::normalized_mask(octants[parent].child_mask);  // C21
         const bool present = (mask >> cidx) & 1u, leaf = (mask >> (cidx + 8u)) & 1u;
         if (present && t_min <= t_max) {  // :622
             if (leaf && t_min > 0.0f) return done(scale);  // :623-625: the first leaf ends the walk

@@ -610,6 +610,15 @@ static void commit_hit(ctx_t *c, ray_t *r, uint32_t prim, const prim_hit *h) {
     }
 }
 
+/* child mask of an octant in the reader form [C21]: OctantChildIterator reads bit i = present,
+ * bit i+8 = leaf (new_octree.rs:84-100), while Octant::set_mask_for (:160-178), the reference's
+ * only writer, stores ChildType::Octant as bit i+8 alone.  (0,1) is therefore an octant child. */
+static inline uint16_t octant_mask(const ref_scene *s, uint32_t octant) {
+    uint32_t m = s->octant_mask[octant];
+    uint32_t present = m & 0xFFu, high = m >> 8;
+    return (uint16_t)((present | (high & ~present)) | ((present & high) << 8));
+}
+
 /* closest primitive of one leaf list whose hit lies before the cell exit [C1] */
 static int leaf_test(ctx_t *c, const ray_t *r, uint32_t leaf, float t_exit_w, float cell_w, uint32_t *best_prim,
                      prim_hit *best) {
@@ -687,7 +696,7 @@ static int esvo(ctx_t *c, const ray_t *ray, float max_dst_w, uint32_t *hit_prim,
         v3 t_corner = vsub(vmul(pos, t_coef), t_bias);
         float tc_max = vmin3(t_corner);
         uint32_t cidx = idx ^ mirror;
-        uint16_t mask = s->octant_mask[parent];
+        uint16_t mask = octant_mask(s, parent);
         uint32_t payload = s->octant_children[8 * (size_t)parent + cidx];
         c->st.node_fetches++;
         int present = (mask >> cidx) & 1, is_leaf = (mask >> (cidx + 8)) & 1;
@@ -1422,7 +1431,7 @@ void ref_traversal_data(const ref_scene *s, const float ray[6], float max_dst_w,
         v3 t_corner = vsub(vmul(pos, t_coef), t_bias);
         float tc_max = vmin3(t_corner);
         uint32_t cidx = idx ^ mirror;
-        uint16_t mask = s->octant_mask[parent];
+        uint16_t mask = octant_mask(s, parent);
         int present = (mask >> cidx) & 1, is_leaf = (mask >> (cidx + 8)) & 1;
         if (present && t_min <= t_max) {
             if (is_leaf && t_min > 0.0f) break;
