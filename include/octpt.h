@@ -294,6 +294,19 @@ octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t sphere_cou
 octpt_status octpt_build_octree_device(octpt_ctx *ctx, const octpt_sphere *spheres, uint32_t sphere_count,
                                        const octpt_cuboid *cuboids, uint32_t cuboid_count, uint32_t depth,
                                        octpt_octree **out);
+/* Builder options (the _ex forms; the plain forms pass 0).
+ * OCTPT_BUILD_COMPACT: Octant::is_compactable (new_octree.rs:227-233) applied bottom-up at every
+ * level, as RegionOctreeBuilder::recursive_build does (:679-690): an octant whose eight children are
+ * leaves holding the same primitive list becomes one leaf of its parent with child 0's payload (the
+ * other seven leaf table entries stay, unreferenced).  The root is never merged away (a Lod root
+ * stays one octant of eight equal leaves, :534-545).  Host and device builds stay equal array for
+ * array. */
+#define OCTPT_BUILD_COMPACT 0x1u
+octpt_status octpt_build_octree_ex(const octpt_sphere *spheres, uint32_t sphere_count, const octpt_cuboid *cuboids,
+                                   uint32_t cuboid_count, uint32_t depth, uint32_t flags, octpt_octree **out);
+octpt_status octpt_build_octree_device_ex(octpt_ctx *ctx, const octpt_sphere *spheres, uint32_t sphere_count,
+                                          const octpt_cuboid *cuboids, uint32_t cuboid_count, uint32_t depth,
+                                          uint32_t flags, octpt_octree **out);
 octpt_status octpt_octree_get_view(const octpt_octree *tree, octpt_octree_view *view);
 void octpt_octree_free(octpt_octree *tree);
 

@@ -30,6 +30,7 @@ RENDER_SHARD_COMPACT = 0x1
 RENDER_MEGAKERNEL = 0x2
 RENDER_KERNEL_TIMING = 0x4
 RENDER_PREVIEW = 0x8
+BUILD_COMPACT = 0x1  # OCTPT_BUILD_COMPACT
 PRIM_NONE = 0xFFFFFFFF
 PRIM_CUBOID_BIT = 0x80000000
 
@@ -176,6 +177,8 @@ SIGNATURES = {
     "octpt_reset_stats": (_i32, [_vp]),
     "octpt_build_octree": (_i32, [_vp, _u32, _vp, _u32, _u32, C.POINTER(_vp)]),
     "octpt_build_octree_device": (_i32, [_vp, _vp, _u32, _vp, _u32, _u32, C.POINTER(_vp)]),
+    "octpt_build_octree_ex": (_i32, [_vp, _u32, _vp, _u32, _u32, _u32, C.POINTER(_vp)]),
+    "octpt_build_octree_device_ex": (_i32, [_vp, _vp, _u32, _vp, _u32, _u32, _u32, C.POINTER(_vp)]),
     "octpt_octree_get_view": (_i32, [_vp, C.POINTER(OctreeView)]),
     "octpt_octree_free": (None, [_vp]),
 }

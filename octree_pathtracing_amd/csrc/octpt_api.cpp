@@ -682,11 +682,26 @@ struct CellPrim {
     bool operator<(const CellPrim &o) const { return code != o.code ? code < o.code : prim < o.prim; }
 };
 
+// Pre-order octant emission.  node() returns the child its parent stores: an octant
+// id, or with compaction a leaf payload when the octant's eight children are leaves holding the same
+// primitive list (Octant::is_compactable, new_octree.rs:227-233, applied bottom-up at every level as
+// RegionOctreeBuilder::recursive_build does, :679-690: the octant becomes Lod(get_child(0))).  The
+// root is never merged away (a Lod root stays one octant of eight equal leaves, :534-545).
 struct Builder {
     octpt_octree *t;
     std::vector<uint64_t> leaf_code;
     uint32_t depth;
-    uint32_t node(uint32_t level, uint32_t lo, uint32_t hi) {
+    bool compact;
+    struct Child {
+        bool leaf;
+        uint32_t v;
+    };
+    bool same_leaf(uint32_t a, uint32_t b) const {
+        const uint32_t n = t->leaf_count[a];
+        return n == t->leaf_count[b] &&
+               std::memcmp(&t->leaf_prims[t->leaf_first[a]], &t->leaf_prims[t->leaf_first[b]], n * sizeof(uint32_t)) == 0;
+    }
+    Child node(uint32_t level, uint32_t lo, uint32_t hi) {
         const uint32_t id = (uint32_t)t->octants.size();
         t->octants.push_back(octpt_octant{0, 0, {0, 0, 0, 0, 0, 0, 0, 0}});
         const uint32_t shift = 3 * (depth - 1 - level);
@@ -699,13 +714,23 @@ struct Builder {
                 t->octants[id].child_mask |= (uint16_t)((1u << c) | (1u << (c + 8)));
                 t->octants[id].children[c] = a;
             } else {
-                const uint32_t ch = node(level + 1, a, b);
-                t->octants[id].child_mask |= (uint16_t)(1u << c);
-                t->octants[id].children[c] = ch;
+                const Child ch = node(level + 1, a, b);
+                t->octants[id].child_mask |= (uint16_t)(ch.leaf ? ((1u << c) | (1u << (c + 8))) : (1u << c));
+                t->octants[id].children[c] = ch.v;
             }
             a = b;
         }
-        return id;
+        if (compact && level > 0 && t->octants[id].child_mask == 0xFFFFu) {
+            const uint32_t *ch = t->octants[id].children;
+            bool same = true;
+            for (int k = 1; k < 8 && same; ++k) same = same_leaf(ch[0], ch[k]);
+            if (same) {  // all children are leaves: this octant is the last one emitted
+                const uint32_t v = ch[0];
+                t->octants.pop_back();
+                return Child{true, v};
+            }
+        }
+        return Child{false, id};
     }
 };
 
@@ -1317,8 +1342,15 @@ octpt_status octpt_reset_stats(octpt_ctx *ctx) {
 
 octpt_status octpt_build_octree_device(octpt_ctx *ctx, const octpt_sphere *spheres, uint32_t ns,
                                        const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, octpt_octree **out) {
+    return octpt_build_octree_device_ex(ctx, spheres, ns, cuboids, nc, depth, 0u, out);
+}
+
+octpt_status octpt_build_octree_device_ex(octpt_ctx *ctx, const octpt_sphere *spheres, uint32_t ns,
+                                          const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, uint32_t flags,
+                                          octpt_octree **out) {
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
     if (!out) return fail(ctx, OCTPT_ERR_INVALID_ARG, "out NULL");
+    if (flags & ~OCTPT_BUILD_COMPACT) return fail(ctx, OCTPT_ERR_INVALID_ARG, "unknown build flags");
     *out = nullptr;
     if (depth < 1 || depth > kMaxDepth) return fail(ctx, OCTPT_ERR_INVALID_ARG, "depth must be in [1, 21]");
     if ((ns && !spheres) || (nc && !cuboids)) return fail(ctx, OCTPT_ERR_INVALID_ARG, "NULL primitive array");
@@ -1331,7 +1363,7 @@ octpt_status octpt_build_octree_device(octpt_ctx *ctx, const octpt_sphere *spher
         bool too_many = false;
         float ms = 0.0f;
         const hipError_t e = build_octree_gpu(ctx->stream, ctx->build_scratch, spheres, ns, cuboids, nc, depth,
-                                              kMaxBuildPairs, *t, too_many, &ms);
+                                              (flags & OCTPT_BUILD_COMPACT) != 0, kMaxBuildPairs, *t, too_many, &ms);
         if (e != hipSuccess || too_many) {
             delete t;
             if (e == hipErrorOutOfMemory || too_many) return fail(ctx, OCTPT_ERR_OOM, "octree build: out of memory");
@@ -1349,7 +1381,13 @@ octpt_status octpt_build_octree_device(octpt_ctx *ctx, const octpt_sphere *spher
 
 octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const octpt_cuboid *cuboids, uint32_t nc,
                                 uint32_t depth, octpt_octree **out) {
+    return octpt_build_octree_ex(spheres, ns, cuboids, nc, depth, 0u, out);
+}
+
+octpt_status octpt_build_octree_ex(const octpt_sphere *spheres, uint32_t ns, const octpt_cuboid *cuboids, uint32_t nc,
+                                   uint32_t depth, uint32_t flags, octpt_octree **out) {
     if (!out) return OCTPT_ERR_INVALID_ARG;
+    if (flags & ~OCTPT_BUILD_COMPACT) return OCTPT_ERR_INVALID_ARG;
     *out = nullptr;
     if (depth < 1 || depth > kMaxDepth) return OCTPT_ERR_INVALID_ARG;
     if ((ns && !spheres) || (nc && !cuboids)) return OCTPT_ERR_INVALID_ARG;
@@ -1418,8 +1456,8 @@ octpt_status octpt_build_octree(const octpt_sphere *spheres, uint32_t ns, const 
             t->leaf_count.back()++;
             t->leaf_prims[k] = cells[k].prim;
         }
-        Builder b{t, std::move(codes), depth};
-        t->root = b.node(0, 0, (uint32_t)b.leaf_code.size());
+        Builder b{t, std::move(codes), depth, (flags & OCTPT_BUILD_COMPACT) != 0};
+        t->root = b.node(0, 0, (uint32_t)b.leaf_code.size()).v;
         *out = t;
         return OCTPT_OK;
     } catch (const std::bad_alloc &) {

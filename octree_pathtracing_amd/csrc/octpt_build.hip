@@ -187,7 +187,8 @@ __global__ __launch_bounds__(kBuildBlock) void link_kernel(const uint64_t *__res
                                                            const uint32_t *__restrict__ base,
                                                            const uint32_t *__restrict__ opens, uint32_t L,
                                                            uint32_t depth, uint32_t *__restrict__ child,
-                                                           uint32_t *__restrict__ mask) {
+                                                           uint32_t *__restrict__ mask, uint32_t *__restrict__ up,
+                                                           uint8_t *__restrict__ lvl) {
     const uint32_t j = blockIdx.x * kBuildBlock + threadIdx.x;
     if (j >= L) return;
     const uint64_t code = leaf_code[j];
@@ -199,11 +200,71 @@ __global__ __launch_bounds__(kBuildBlock) void link_kernel(const uint64_t *__res
         const uint32_t c = (uint32_t)(code >> (3u * (depth - level))) & 7u;
         child[8u * parent + c] = id;
         atomicOr(&mask[parent], 1u << c);
+        if (up) {  // compaction: parent slot and level
+            up[id] = 8u * parent + c;
+            lvl[id] = (uint8_t)level;
+        }
     }
     const uint32_t p = nj ? base[j] + nj - 1u : octant_at(leaf_code, base, opens, L, depth, depth - 1u, code);
     const uint32_t c = (uint32_t)code & 7u;
     child[8u * p + c] = j;  // leaf payload = leaf table index
     atomicOr(&mask[p], (1u << c) | (1u << (c + 8u)));
+}
+
+// Compaction (OCTPT_BUILD_COMPACT), one launch per level bottom-up: a level-`level` octant whose
+// eight children are leaves holding the same primitive list becomes a leaf of its parent with child
+// 0's payload (Octant::is_compactable, new_octree.rs:227-233; RegionOctreeBuilder::recursive_build
+// :679-690).  Parents are one level up, handled by the next launch; siblings touch distinct slots.
+// up[o] = the parent slot (8 * parent + child index), lvl[o] its level; the root (level 0) stays.
+__global__ __launch_bounds__(kBuildBlock) void compact_level_kernel(const uint32_t *__restrict__ up,
+                                                                    const uint8_t *__restrict__ lvl, uint32_t n_oct,
+                                                                    uint32_t level, const uint32_t *__restrict__ leaf_first,
+                                                                    const uint32_t *__restrict__ leaf_count,
+                                                                    const uint32_t *__restrict__ prims,
+                                                                    uint32_t *__restrict__ child,
+                                                                    uint32_t *__restrict__ mask,
+                                                                    uint32_t *__restrict__ keep) {
+    const uint32_t o = blockIdx.x * kBuildBlock + threadIdx.x;
+    if (o == 0u || o >= n_oct) return;  // octant 0 is the root
+    if (lvl[o] != level || mask[o] != 0xFFFFu) return;
+    const uint32_t c0 = child[8u * o];
+    const uint32_t f0 = leaf_first[c0], n0 = leaf_count[c0];
+    for (int k = 1; k < 8; ++k) {
+        const uint32_t ck = child[8u * o + k];
+        if (leaf_count[ck] != n0) return;
+        const uint32_t fk = leaf_first[ck];
+        for (uint32_t e = 0; e < n0; ++e)
+            if (prims[fk + e] != prims[f0 + e]) return;
+    }
+    keep[o] = 0u;
+    const uint32_t slot = up[o];
+    child[slot] = c0;
+    atomicOr(&mask[slot >> 3], 1u << ((slot & 7u) + 8u));
+}
+
+// surviving octants in pre-order: new id = exclusive scan of keep; octant children renumbered
+__global__ __launch_bounds__(kBuildBlock) void pack_compacted_kernel(const uint32_t *__restrict__ child,
+                                                                     const uint32_t *__restrict__ mask,
+                                                                     const uint32_t *__restrict__ keep,
+                                                                     const uint32_t *__restrict__ new_id, uint32_t n,
+                                                                     octpt_octant *__restrict__ out) {
+    const uint32_t o = blockIdx.x * kBuildBlock + threadIdx.x;
+    if (o >= n || !keep[o]) return;
+    octpt_octant v;
+    const uint32_t m = mask[o];
+    v.child_mask = (uint16_t)m;
+    v.reserved = 0;
+    for (int c = 0; c < 8; ++c) {
+        const uint32_t x = child[8u * o + c];
+        v.children[c] = ((m >> c) & 1u) && !((m >> (c + 8)) & 1u) ? new_id[x] : x;
+    }
+    out[new_id[o]] = v;
+}
+
+// keep[i] = 1 for i < n_ones, 0 for the scan's trailing entry
+__global__ __launch_bounds__(kBuildBlock) void fill_u32_kernel(uint32_t *__restrict__ a, uint32_t n, uint32_t n_ones) {
+    const uint32_t i = blockIdx.x * kBuildBlock + threadIdx.x;
+    if (i < n) a[i] = i < n_ones ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kBuildBlock) void pack_octants_kernel(const uint32_t *__restrict__ child,
@@ -262,8 +323,8 @@ void BuildScratch::release() {
 }
 
 hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const octpt_sphere *spheres, uint32_t ns,
-                            const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, uint64_t max_pairs,
-                            BuiltOctree &out, bool &too_many, float *ms) {
+                            const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, bool compact,
+                            uint64_t max_pairs, BuiltOctree &out, bool &too_many, float *ms) {
     too_many = false;
     const int32_t N = 1 << depth;
     const uint32_t np = ns + nc;
@@ -362,19 +423,48 @@ hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const oct
     uint32_t n_oct = 0;
     BTRY(hipMemcpyAsync(&n_oct, d_base + L, sizeof n_oct, hipMemcpyDeviceToHost, stream));
     BTRY(hipStreamSynchronize(stream));
-    uint32_t *d_child, *d_mask;
+    uint32_t *d_child, *d_mask, *d_up = nullptr, *d_keep = nullptr, *d_newid = nullptr;
+    uint8_t *d_lvl = nullptr;
     octpt_octant *d_oct;
     BTRY(pool.get(&d_child, (size_t)n_oct * 8));
     BTRY(pool.get(&d_mask, n_oct));
     BTRY(pool.get(&d_oct, n_oct));
+    if (compact) {
+        BTRY(pool.get(&d_up, n_oct));
+        BTRY(pool.get(&d_lvl, n_oct));
+        BTRY(pool.get(&d_keep, n_oct + 1));  // entry n_oct = 0: the exclusive scan's last input
+        BTRY(pool.get(&d_newid, n_oct + 1));
+    }
     BTRY(hipMemsetAsync(d_child, 0, (size_t)n_oct * 8 * sizeof(uint32_t), stream));
     BTRY(hipMemsetAsync(d_mask, 0, (size_t)n_oct * sizeof(uint32_t), stream));
     hipLaunchKernelGGL(link_kernel, dim3(blocks(L)), dim3(kBuildBlock), 0, stream, d_lcode, d_base, d_opens, L, depth,
-                       d_child, d_mask);
+                       d_child, d_mask, d_up, d_lvl);
     BTRY(hipGetLastError());
-    hipLaunchKernelGGL(pack_octants_kernel, dim3(blocks(n_oct)), dim3(kBuildBlock), 0, stream, d_child, d_mask, n_oct,
-                       d_oct);
-    BTRY(hipGetLastError());
+    if (compact) {
+        // keep = 1 per octant, then one pass per level, bottom-up
+        hipLaunchKernelGGL(fill_u32_kernel, dim3(blocks(n_oct + 1)), dim3(kBuildBlock), 0, stream, d_keep, n_oct + 1,
+                           n_oct);
+        BTRY(hipGetLastError());
+        for (uint32_t level = depth - 1; level >= 1; --level) {
+            hipLaunchKernelGGL(compact_level_kernel, dim3(blocks(n_oct)), dim3(kBuildBlock), 0, stream, d_up, d_lvl, n_oct,
+                               level, d_first, d_count, d_prim_s, d_child, d_mask, d_keep);
+            BTRY(hipGetLastError());
+        }
+        size_t id_bytes = 0;
+        BTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, id_bytes, d_keep, d_newid, n_oct + 1, stream));
+        char *d_tmp3;
+        BTRY(pool.get(&d_tmp3, id_bytes));
+        BTRY(hipcub::DeviceScan::ExclusiveSum(d_tmp3, id_bytes, d_keep, d_newid, n_oct + 1, stream));
+        hipLaunchKernelGGL(pack_compacted_kernel, dim3(blocks(n_oct)), dim3(kBuildBlock), 0, stream, d_child, d_mask,
+                           d_keep, d_newid, n_oct, d_oct);
+        BTRY(hipGetLastError());
+        BTRY(hipMemcpyAsync(&n_oct, d_newid + n_oct, sizeof n_oct, hipMemcpyDeviceToHost, stream));
+        BTRY(hipStreamSynchronize(stream));
+    } else {
+        hipLaunchKernelGGL(pack_octants_kernel, dim3(blocks(n_oct)), dim3(kBuildBlock), 0, stream, d_child, d_mask,
+                           n_oct, d_oct);
+        BTRY(hipGetLastError());
+    }
     BTRY(hipEventRecord(e1, stream));
     out.octants.resize(n_oct);
     out.leaf_first.resize(L);

@@ -246,7 +246,7 @@ struct BuiltOctree {
 // grow-only device scratch of the GPU octree builder, owned by the context: repeated builds
 // (scene edits) reuse it instead of paying hipMalloc / hipFree per buffer
 struct BuildScratch {
-    static constexpr int kSlots = 24;
+    static constexpr int kSlots = 32;
     void *dev[kSlots] = {};
     size_t cap[kSlots] = {};
     void release();
@@ -254,7 +254,7 @@ struct BuildScratch {
 
 // the octree builder on the device (octpt_build.hip); too_many: more than max_pairs pairs
 hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const octpt_sphere *spheres, uint32_t ns,
-                            const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, uint64_t max_pairs,
-                            BuiltOctree &out, bool &too_many, float *ms);
+                            const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, bool compact,
+                            uint64_t max_pairs, BuiltOctree &out, bool &too_many, float *ms);
 
 }  // namespace octpt

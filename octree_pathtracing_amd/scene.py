@@ -211,19 +211,22 @@ class Scene:
     octree: Octree | None = None
 
     # ---------------------------------------------------------------- octree
-    def build_octree(self, depth: int, renderer=None) -> Octree:
+    def build_octree(self, depth: int, renderer=None, compact: bool = False) -> Octree:
         """Voxelise the primitives with the product builder: octpt_build_octree (host), or with a
-        HipRenderer given, octpt_build_octree_device on its GPU (the same arrays)."""
+        HipRenderer given, octpt_build_octree_device on its GPU (the same arrays).  compact: merge
+        eight sibling leaves holding the same primitive list, bottom-up (OCTPT_BUILD_COMPACT,
+        Octant::is_compactable, new_octree.rs:227-233)."""
         lib = _lib.load()
         sph = self.sphere_structs()
         cub = self.cuboid_structs()
         handle = C.c_void_p()
         args = (C.cast(sph, C.c_void_p) if len(self.spheres) else None, len(self.spheres),
-                C.cast(cub, C.c_void_p) if len(self.cuboids) else None, len(self.cuboids), depth, C.byref(handle))
+                C.cast(cub, C.c_void_p) if len(self.cuboids) else None, len(self.cuboids), depth,
+                _lib.BUILD_COMPACT if compact else 0, C.byref(handle))
         if renderer is None:
-            _lib.check(lib, None, lib.octpt_build_octree(*args))
+            _lib.check(lib, None, lib.octpt_build_octree_ex(*args))
         else:
-            _lib.check(lib, renderer._ctx, lib.octpt_build_octree_device(renderer._ctx, *args))
+            _lib.check(lib, renderer._ctx, lib.octpt_build_octree_device_ex(renderer._ctx, *args))
         try:
             v = _lib.OctreeView()
             _lib.check(lib, None, lib.octpt_octree_get_view(handle, C.byref(v)))

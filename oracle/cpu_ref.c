@@ -1589,6 +1589,8 @@ typedef struct {
     uint32_t n, cap;
     const uint64_t *leaf_code;
     uint32_t depth;
+    int compact; /* REF_BUILD_COMPACT: Octant::is_compactable merge (new_octree.rs:227-233) */
+    const uint32_t *leaf_first, *leaf_count, *leaf_prims;
 } tree_build;
 
 static int tb_alloc(tree_build *tb) {
@@ -1607,7 +1609,19 @@ static int tb_alloc(tree_build *tb) {
     memset(&tb->child[8 * (size_t)id], 0, 8 * sizeof(uint32_t));
     return (int)id;
 }
-static int tb_node(tree_build *tb, uint32_t level, uint32_t lo, uint32_t hi) {
+/* two leaves hold the same primitive list (the leaf-value equality of is_compactable) */
+static int same_leaf(const tree_build *tb, uint32_t a, uint32_t b) {
+    if (tb->leaf_count[a] != tb->leaf_count[b]) return 0;
+    return memcmp(&tb->leaf_prims[tb->leaf_first[a]], &tb->leaf_prims[tb->leaf_first[b]],
+                  tb->leaf_count[a] * sizeof(uint32_t)) == 0;
+}
+/* Pre-order octant emission of the leaves [lo, hi) below a level-`level` octant.  Returns the
+ * child the parent stores: *is_leaf = 0 with the octant id, or, with compaction, *is_leaf = 1 and
+ * a leaf payload when all eight children are leaves holding the same list -- Octant::
+ * is_compactable (new_octree.rs:227-233) as RegionOctreeBuilder::recursive_build applies it at
+ * every level (:679-690): the octant becomes Lod(get_child(0)) in its parent.  The root is never
+ * merged away (a Lod root stays an octant of eight equal leaves, :534-545).  -1 = out of memory. */
+static int tb_node(tree_build *tb, uint32_t level, uint32_t lo, uint32_t hi, int *is_leaf, uint32_t *value) {
     int id = tb_alloc(tb);
     if (id < 0) return -1;
     uint32_t shift = 3 * (tb->depth - 1 - level);
@@ -1620,18 +1634,31 @@ static int tb_node(tree_build *tb, uint32_t level, uint32_t lo, uint32_t hi) {
             tb->mask[id] |= (uint16_t)((1u << cidx) | (1u << (cidx + 8)));
             tb->child[8 * (size_t)id + cidx] = a; /* leaf payload = leaf index */
         } else {
-            int ch = tb_node(tb, level + 1, a, b);
-            if (ch < 0) return -1;
-            tb->mask[id] |= (uint16_t)(1u << cidx);
-            tb->child[8 * (size_t)id + cidx] = (uint32_t)ch;
+            int leaf;
+            uint32_t v;
+            if (tb_node(tb, level + 1, a, b, &leaf, &v) < 0) return -1;
+            tb->mask[id] |= (uint16_t)(leaf ? ((1u << cidx) | (1u << (cidx + 8))) : (1u << cidx));
+            tb->child[8 * (size_t)id + cidx] = v;
         }
         a = b;
     }
-    return id;
+    *is_leaf = 0;
+    *value = (uint32_t)id;
+    if (tb->compact && level > 0 && tb->mask[id] == 0xFFFFu) {
+        const uint32_t *ch = &tb->child[8 * (size_t)id];
+        int same = 1;
+        for (int k = 1; k < 8 && same; k++) same = same_leaf(tb, ch[0], ch[k]);
+        if (same) { /* all children are leaves, so this octant is the last one emitted */
+            *is_leaf = 1;
+            *value = ch[0];
+            tb->n--;
+        }
+    }
+    return 0;
 }
 
 int ref_build_octree(const float *spheres, uint32_t ns, const float *cuboids, uint32_t nc, uint32_t depth,
-                     ref_octree *out) {
+                     uint32_t flags, ref_octree *out) {
     memset(out, 0, sizeof *out);
     if (depth < 1 || depth > 21) return 1;
     int32_t N = 1 << depth;
@@ -1711,9 +1738,15 @@ int ref_build_octree(const float *spheres, uint32_t ns, const float *cuboids, ui
     tree_build tb = {0};
     tb.leaf_code = codes;
     tb.depth = depth;
-    int root = tb_node(&tb, 0, 0, nleaves);
+    tb.compact = (flags & REF_BUILD_COMPACT) != 0;
+    tb.leaf_first = out->leaf_first;
+    tb.leaf_count = out->leaf_count;
+    tb.leaf_prims = out->leaf_prims;
+    int root_leaf;
+    uint32_t root;
+    int rc = tb_node(&tb, 0, 0, nleaves, &root_leaf, &root);
     free(codes);
-    if (root < 0) { free(tb.mask); free(tb.child); goto oom; }
+    if (rc < 0) { free(tb.mask); free(tb.child); goto oom; }
     out->octant_mask = tb.mask;
     out->octant_children = tb.child;
     out->n_octants = tb.n;

@@ -154,8 +154,11 @@ typedef struct {
     uint32_t *leaf_first, *leaf_count, *leaf_prims;
     uint32_t n_leaves, n_leaf_prims;
 } ref_octree;
+/* flags: REF_BUILD_COMPACT merges eight sibling leaves holding the same primitive list into one
+ * leaf a level up, bottom-up (Octant::is_compactable, new_octree.rs:227-233) */
+#define REF_BUILD_COMPACT 0x1u
 int ref_build_octree(const float *spheres, uint32_t n_spheres, const float *cuboids, uint32_t n_cuboids,
-                     uint32_t depth, ref_octree *out);
+                     uint32_t depth, uint32_t flags, ref_octree *out);
 void ref_free_octree(ref_octree *t);
 
 /* --- closest-hit query (Scene::hit), one ray per entry ---

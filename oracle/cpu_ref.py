@@ -109,7 +109,7 @@ def load() -> C.CDLL:
     lib.ref_morton_lut_selftest.restype = C.c_uint64
     lib.ref_morton_lut_selftest.argtypes = [u32]
     lib.ref_build_octree.restype = C.c_int
-    lib.ref_build_octree.argtypes = [vp, u32, vp, u32, u32, C.POINTER(RefOctree)]
+    lib.ref_build_octree.argtypes = [vp, u32, vp, u32, u32, u32, C.POINTER(RefOctree)]
     lib.ref_free_octree.restype = None
     lib.ref_free_octree.argtypes = [C.POINTER(RefOctree)]
     lib.ref_intersect.restype = None
@@ -139,13 +139,14 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None
 
 
-def build_octree(spheres: np.ndarray, cuboids: np.ndarray, depth: int):
-    """Oracle builder -> dict of numpy arrays (octant_mask, octant_children, root, depth, leaf_*)."""
+def build_octree(spheres: np.ndarray, cuboids: np.ndarray, depth: int, compact: bool = False):
+    """Oracle builder -> dict of numpy arrays (octant_mask, octant_children, root, depth, leaf_*).
+    compact: merge eight equal sibling leaves bottom-up (Octant::is_compactable, new_octree.rs:227-233)."""
     lib = load()
     sp = np.ascontiguousarray(spheres, np.float32).reshape(-1, 4)
     cb = np.ascontiguousarray(cuboids, np.float32).reshape(-1, 6)
     t = RefOctree()
-    rc = lib.ref_build_octree(_p(sp), len(sp), _p(cb), len(cb), depth, C.byref(t))
+    rc = lib.ref_build_octree(_p(sp), len(sp), _p(cb), len(cb), depth, 1 if compact else 0, C.byref(t))
     if rc != 0:
         raise RuntimeError(f"ref_build_octree failed ({rc})")
     try:

@@ -110,3 +110,73 @@ def test_unit_blocks_claim_one_cell():
     t = _same(sc)
     assert len(t.leaf_first) == 1 + 1 + 3  # x cells 0,1,2 for the third box
     assert np.all(t.leaf_count == 1)
+
+
+# ----------------------------------------------------------------------------- compaction (OCTPT_BUILD_COMPACT)
+def _same_compact(sc, depth):
+    t = sc.build_octree(depth, compact=True)
+    ref = cpu_ref.build_octree(sc.spheres, sc.cuboids, depth, compact=True)
+    for k in ("octant_mask", "octant_children", "leaf_first", "leaf_count", "leaf_prims"):
+        assert np.array_equal(ref[k], getattr(t, k)), k
+    assert ref["root"] == t.root
+    return t
+
+
+def _no_compactable_octant(t):
+    """Octant::is_compactable (new_octree.rs:227-233) holds for no octant but the root: eight
+    leaves with equal lists never survive below it."""
+    lists = [tuple(t.leaf_prims[f:f + c]) for f, c in zip(t.leaf_first, t.leaf_count)]
+    for n in range(t.octant_count):
+        if n == t.root or int(t.octant_mask[n]) != 0xFFFF:
+            continue
+        assert len({lists[int(v)] for v in t.octant_children[n]}) > 1
+
+
+@pytest.mark.parametrize("name", ["tiny", "C2", "C3", "C5", "blocks"])
+def test_compact_builder_configs(name):
+    sc, _, _ = S.make_config(name)
+    full = sc.octree
+    t = _same_compact(sc, full.depth)
+    _no_compactable_octant(t)
+    assert t.octant_count <= full.octant_count
+    # the leaf tables are the uncompacted ones (merged-away entries stay, unreferenced)
+    assert np.array_equal(t.leaf_first, full.leaf_first) and np.array_equal(t.leaf_prims, full.leaf_prims)
+
+
+def test_compact_merges_solid_blocks():
+    """A solid 4x4x4 block of one cuboid: the unit cells merge twice (two levels up), and a 2x2x2
+    block beside it once; a lone cell stays at the bottom."""
+    sc = S.Scene()
+    sc.cuboids = np.array([[0, 0, 0, 4, 4, 4], [8, 0, 0, 10, 2, 2], [12, 12, 12, 13, 13, 13]], np.float32)
+    sc.cuboid_material = np.zeros((3, 6), np.uint32)
+    t = _same_compact(sc, 4)
+    from tests.octree_forms import leaf_levels
+    assert leaf_levels(t) == {2: 1, 1: 1, 0: 1}
+    # root + one octant above block 0's leaf + two above block 1's + three above the lone cell
+    assert t.octant_count == 1 + 1 + 2 + 3
+
+
+@pytest.mark.parametrize("seed,depth", [(5, 3), (6, 6), (7, 9)])
+def test_compact_random_closest_hits(seed, depth):
+    """A compacted tree answers closest-hit queries as the full tree does wherever leaves merged
+    (same primitives, tested once in the larger cell), and both match brute force."""
+    world = float(1 << depth)
+    sc = S.Scene()
+    sc.spheres = S.random_spheres(seed, 40, world, 0.5, max(world / 4, 1.0))
+    sc.sphere_material = np.zeros(40, np.uint32)
+    sc.cuboids = S.random_cuboids(seed, 20, world, 0.5, max(world / 3, 1.0))
+    sc.cuboid_material = np.zeros((20, 6), np.uint32)
+    t = _same_compact(sc, depth)
+    _no_compactable_octant(t)
+    rng = np.random.default_rng(seed)
+    m = 2000
+    o = rng.uniform(0.01, world - 0.01, (m, 3)).astype(np.float32)
+    d = rng.normal(size=(m, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True).astype(np.float32)
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    tc, pc, _, sc_steps = cpu_ref.intersect(sc, rays)
+    tb, pb = cpu_ref.intersect_brute(sc, rays)
+    p = o + d * np.where(np.isfinite(tb), tb, 0)[:, None]
+    visible = ~np.isfinite(tb) | np.all((p >= 0) & (p < world), axis=1)
+    agree = (pc == pb) & ((tc == tb) | ~np.isfinite(tb))
+    assert agree[visible].mean() > 0.995

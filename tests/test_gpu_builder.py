@@ -19,9 +19,9 @@ def renderer():
     r.close()
 
 
-def _same(sc, depth, renderer):
-    host = sc.build_octree(depth)
-    dev = sc.build_octree(depth, renderer=renderer)
+def _same(sc, depth, renderer, compact=False):
+    host = sc.build_octree(depth, compact=compact)
+    dev = sc.build_octree(depth, renderer=renderer, compact=compact)
     assert dev.root == host.root and dev.depth == host.depth
     for k in ("octant_mask", "octant_children", "leaf_first", "leaf_count", "leaf_prims"):
         assert np.array_equal(getattr(dev, k), getattr(host, k)), k
@@ -64,3 +64,30 @@ def test_device_builder_empty_and_oom(renderer):
     with pytest.raises(_lib.OctptError) as e:
         big.build_octree(11, renderer=renderer)
     assert e.value.status == _lib.ERR_OOM
+
+
+@pytest.mark.parametrize("name", ["tiny", "C2", "C3", "C4", "C5"])
+def test_device_builder_compact_configs(renderer, name):
+    """OCTPT_BUILD_COMPACT (Octant::is_compactable bottom-up, new_octree.rs:227-233): the device's
+    level-by-level merge and renumbering equal the host's recursive merge array for array."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, _, _ = S.make_config(name, build=False)
+    full = sc.build_octree(sc._depth)
+    t = _same(sc, sc._depth, renderer, compact=True)
+    assert t.octant_count <= full.octant_count
+
+
+@pytest.mark.parametrize("seed,depth", [(6, 2), (7, 5), (8, 8), (9, 12)])
+def test_device_builder_compact_random(renderer, seed, depth):
+    from octree_pathtracing_amd import scene as S
+
+    world = float(1 << depth)
+    sc = S.Scene()
+    sc.spheres = S.random_spheres(seed, 200, world, 0.5, max(world / 5, 1.0))
+    sc.sphere_material = np.zeros(200, np.uint32)
+    sc.cuboids = np.floor(S.random_cuboids(seed, 60, world, 1.0, max(world / 3, 2.0)))  # solid integer blocks merge
+    sc.cuboid_material = np.zeros((60, 6), np.uint32)
+    full = sc.build_octree(depth)
+    t = _same(sc, depth, renderer, compact=True)
+    assert t.octant_count < full.octant_count

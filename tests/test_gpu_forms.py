@@ -78,3 +78,17 @@ def test_intersect_mixed_levels(torch_cuda, renderer, name, levels):
     assert np.array_equal(prim, rprim) and np.array_equal(steps, rsteps)
     assert np.array_equal(t, rt) and np.array_equal(nrm, rnrm)
     assert (prim != 0xFFFFFFFF).mean() > 0.3
+
+
+@pytest.mark.parametrize("name,res", [("C3", (192, 108, 2)), ("C4", (128, 72, 2)), ("C2", (160, 90, 4))])
+def test_compacted_tree_parity(torch_cuda, renderer, name, res):
+    """A tree built with OCTPT_BUILD_COMPACT (merged LOD leaves one and two levels up) renders as the
+    oracle renders the same tree."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config(name)
+    rs.width, rs.height, rs.spp = res
+    sc.build_octree(sc.octree.depth, compact=True)
+    h = leaf_levels(sc.octree)
+    assert max(h) >= 1, h
+    assert_parity(gpu_render(torch_cuda, renderer, sc, cam, rs), oracle(sc, cam, rs, forward=True), f"{name} compact")
