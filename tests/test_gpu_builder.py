@@ -84,7 +84,7 @@ def test_device_builder_compact_random(renderer, seed, depth):
 
     world = float(1 << depth)
     sc = S.Scene()
-    sc.spheres = S.random_spheres(seed, 200, world, 0.5, max(world / 5, 1.0))
+    sc.spheres = S.random_spheres(seed, 200, world, 0.5, min(max(world / 5, 1.0), 24.0))
     sc.sphere_material = np.zeros(200, np.uint32)
     sc.cuboids = np.floor(S.random_cuboids(seed, 60, world, 1.0, min(max(world / 3, 2.0), 48.0)))  # solid blocks merge
     sc.cuboid_material = np.zeros((60, 6), np.uint32)
