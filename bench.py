@@ -6,7 +6,9 @@ A step = one full progressive render of the frame (all 256 passes of every pixel
 scene resident in HBM.  With N > 1 GPUs (torchrun, one process per GPU) the frame is split
 into 8x8 tiles dealt round-robin to ranks (strong scaling: the frame is fixed), each rank
 renders its tiles into a compact buffer and the tiles are gathered to rank 0 over RCCL
-(all_gather_into_tensor) and scattered into the frame by octpt_unshard_device.
+(dist.gather) and scattered into the frame by octpt_unshard_device.  `--gpus N` started without
+torchrun spawns the N ranks itself (octree_pathtracing_amd/launch.py) before anything touches the
+GPU; under torchrun WORLD_SIZE must equal N.
 
 value = total ray segments (closest-hit queries, all ranks) / wall time of the K timed steps
 (max over ranks).  roofline: the dominant kernel is wf_extend_kernel (octree traversal +
@@ -14,8 +16,10 @@ primitive tests, ~90 % of GPU time); achieved = its algorithmic bytes per launch
 / its average launch duration, both measured live: every extend / shade launch of the timed
 steps is bracketed by HIP events on the render stream (OCTPT_RENDER_KERNEL_TIMING).  traffic =
 the L2-to-fabric bytes per extend launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-committed in profiles/pmc_<config>.json.  cpu_baseline = the oracle (oracle/cpu_ref.c, a C port
-of the reference's CPU TileRenderer) timed on this host on a bounded sample.
+committed in profiles/pmc_<config>.json (traffic_source names the file and the FETCH_SIZE factor
+calibrated by tools/fetch_calib.hip).  cpu_baseline = the oracle (oracle/cpu_ref.c, a C port of
+the reference's CPU TileRenderer) built -O3 -march=native on this host and timed on a bounded
+sample with the host's CPU share of threads (model, nproc and flags recorded).
 """
 from __future__ import annotations
 
@@ -51,35 +55,73 @@ def shade_bytes(st: dict) -> float:
 
 
 def load_traffic(config: str):
+    """(bytes per extend launch, source description) from profiles/pmc_<config>.json, or (None, None)."""
     p = ROOT / "profiles" / f"pmc_{config}.json"
     if p.exists():
         try:
             d = json.loads(p.read_text())
-            return d.get("wf_extend_kernel", {}).get("bytes_per_launch")
+            b = d.get("wf_extend_kernel", {}).get("bytes_per_launch")
+            return b, f"profiles/pmc_{config}.json: {d.get('correction', '')}"
         except Exception:
-            return None
-    return None
+            return None, None
+    return None, None
 
 
-def cpu_baseline(sc, cam, rs, seconds: float, threads: int) -> dict:
+def host_cpu() -> dict:
+    """The host the CPU baseline runs on: model, logical CPUs, the affinity mask and the thread
+    share used (the box's OMP_NUM_THREADS share when set: a GPU box's nproc shows the whole machine)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    threads = min(aff, int(share)) if share and share.isdigit() and int(share) > 0 else aff
+    return {"model": model, "nproc": os.cpu_count(), "affinity": aff, "threads": threads}
+
+
+def native_oracle():
+    """Build the oracle -O3 -march=native for this host (oracle/Makefile `native`, into oracle/_native/;
+    the x86-64-v2 build stays the parity checker) and return (path, flags), or the portable build."""
+    import subprocess
+
+    try:
+        # -B: always for this host (a library built on another machine's -march=native may not run here)
+        subprocess.run(["make", "-s", "-B", "-C", str(ROOT / "oracle"), "native"], check=True, capture_output=True,
+                       timeout=180)
+        return ROOT / "oracle" / "_native" / "libcpu_ref_native.so", "-O3 -march=native -ffp-contract=off"
+    except Exception:
+        return ROOT / "oracle" / "libcpu_ref.so", "-O2 -march=x86-64-v2 -ffp-contract=off (native build failed)"
+
+
+def cpu_baseline(sc, cam, rs, seconds: float, threads: int | None) -> dict:
     """Oracle on the host cores: whole 1 spp passes of the full frame until `seconds` elapse."""
     from oracle import cpu_ref
 
+    host = host_cpu()
+    n = threads or host["threads"]
+    lib_path, flags = native_oracle()
+    cpu_ref.load(lib_path)
     acc = None
     segs = 0
     passes = 0
     t0 = time.perf_counter()
     while True:
         acc, _, st = cpu_ref.render(sc, cam, rs.width, rs.height, 1, spp_start=passes, max_depth=rs.max_depth,
-                                    seed=rs.seed, threads=threads, accum=acc)
+                                    seed=rs.seed, threads=n, accum=acc)
         segs += st["segments"]
         passes += 1
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": n, "kind": "port",
             "sample": f"{passes} full-frame pass(es) of the same workload ({rs.width}x{rs.height}, 1 spp each, "
-                      f"{segs} segments) in {dt:.1f} s"}
+                      f"{segs} segments) in {dt:.1f} s",
+            "cpu_model": host["model"], "nproc": host["nproc"], "affinity": host["affinity"], "build": flags}
 
 
 def main():
@@ -90,9 +132,18 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=None, help="override passes per step (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None, help="default: the host's CPU share (host_cpu)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: host-staged gather (rehearses N ranks on fewer GPUs); nccl = RCCL over xGMI")
+    ap.add_argument("--dump-frame", default=None, help="rank 0 saves the gathered frame (.npy) after the last step")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU without torchrun: spawn the ranks before anything touches the GPU
+        from octree_pathtracing_amd.launch import spawn_ranks
+
+        sys.exit(spawn_ranks(args.gpus, [str(Path(__file__).resolve()), *sys.argv[1:]]))
 
     import torch
     import torch.distributed as dist
@@ -100,9 +151,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > n_dev:
+        print(f"bench.py: {world} ranks over RCCL need {world} GPUs, {n_dev} visible", file=sys.stderr)
+        sys.exit(2)
+    dev_idx = local % max(n_dev, 1)
+    torch.cuda.set_device(dev_idx)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
 
     from octree_pathtracing_amd import scene as S
     from octree_pathtracing_amd.distributed import gather_frame
@@ -112,25 +175,35 @@ def main():
     if args.spp:
         rs.spp = args.spp
     W, H = rs.width, rs.height
-    r = HipRenderer(device=local)
+    r = HipRenderer(device=dev_idx)
     r.set_scene(sc)
     r.set_camera(cam)
     r.max_depth, r.seed = rs.max_depth, rs.seed
     stride = max(shard_pixels(W, H, i, world) for i in range(world))
     n_local = shard_pixels(W, H, rank, world)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", dev_idx)
+    host_staged = world > 1 and args.dist_backend == "gloo"
     accum = torch.zeros((stride, 4), dtype=torch.float32, device=dev)
     accum[:, 3] = 1.0
-    gbuf = torch.zeros((world * stride, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    gdev = "cpu" if host_staged else dev
+    gbuf = torch.zeros((world * stride, 4), dtype=torch.float32, device=gdev) if (world > 1 and rank == 0) else None
+    gbuf_dev = torch.zeros((world * stride, 4), dtype=torch.float32, device=dev) if (host_staged and rank == 0) else None
     frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev) if (world > 1 and rank == 0) else None
     params = r.params(W, H, 0, rs.spp, rank, world, compact=True, kernel_timing=True)
+
+    def unshard(g):
+        stream = torch.cuda.current_stream().cuda_stream
+        if host_staged:
+            gbuf_dev.copy_(g)
+            g = gbuf_dev
+        r.unshard_device(W, H, world, g.data_ptr(), stride, frame.data_ptr(), stream)
 
     def step():
         stream = torch.cuda.current_stream().cuda_stream
         r.render_device(params, accum.data_ptr(), None, stream)
-        if world > 1:  # RCCL all_gather_into_tensor over xGMI, then the unshard kernel on rank 0
-            gather_frame(accum, gbuf, W, H, rank, world,
-                         lambda g: r.unshard_device(W, H, world, g.data_ptr(), stride, frame.data_ptr(), stream))
+        if world > 1:  # gather to rank 0 (RCCL over xGMI), then the unshard kernel on rank 0
+            src = accum.cpu() if host_staged else accum
+            gather_frame(src, gbuf, W, H, rank, world, unshard)
 
     for _ in range(args.warmup):
         step()
@@ -149,10 +222,11 @@ def main():
     st = r.stats()
     seg = st["segments"]
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        cdev = gdev  # collectives on the backend's device (gloo: host tensors)
+        t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        s = torch.tensor([seg], dtype=torch.float64, device=dev)
+        s = torch.tensor([seg], dtype=torch.float64, device=cdev)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         seg = int(s.item())
 
@@ -163,7 +237,7 @@ def main():
     n_sh = max(st["shade_launches"], 1)
     sh_s = st["shade_ms"] / 1e3 / n_sh
     sh_bytes = shade_bytes(st) / n_sh
-    traffic = load_traffic(args.config)
+    traffic, traffic_src = load_traffic(args.config)
     out = {
         "metric": METRIC,
         "value": round(seg / dt / 1e6, 2),
@@ -182,7 +256,7 @@ def main():
                         f"{sc.octree.depth}, {W}x{H}, {rs.spp} spp, max_depth {rs.max_depth}, seed {rs.seed}",
             "resolution": [W, H],
             "spp": rs.spp,
-            "parallelism": f"tiles{world}" if world > 1 else "single",
+            "parallelism": (f"tiles{world}" + ("-gloo" if host_staged else "")) if world > 1 else "single",
             "paths_per_step": W * H * rs.spp,
             "segments_per_step": seg // max(args.steps, 1),
         },
@@ -193,6 +267,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "wf_extend_kernel",
             "launches": st["extend_launches"],
             "kernel_ms_avg": round(ext_s * 1e3, 4),
@@ -210,6 +285,13 @@ def main():
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
+        if args.dump_frame:  # the frame in image order (a single rank's buffer is tile-major too)
+            if world == 1:
+                frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev)
+                r.unshard_device(W, H, 1, accum.data_ptr(), stride, frame.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            np.save(args.dump_frame, frame.cpu().numpy())
     r.close()
     if world > 1:
         dist.destroy_process_group()

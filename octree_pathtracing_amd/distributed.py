@@ -64,16 +64,16 @@ def unshard_host(shards: np.ndarray, W: int, H: int, N: int, stride: int) -> np.
 
 
 def gather_frame(accum, gbuf, W: int, H: int, rank: int, world: int, unshard):
-    """All-gather the ranks' compact shards (torch tensors [stride, 4]) into gbuf [world * stride, 4]
-    and let rank 0 scatter them into the frame with `unshard(gbuf)`.  On RCCL the gather is one
-    all_gather_into_tensor; on gloo (no tensor-gather) a list all_gather into views of gbuf."""
+    """Gather the ranks' compact shards (tensors [stride, 4]) to rank 0 into gbuf [world * stride, 4]
+    (rank 0 only; None elsewhere) and let rank 0 scatter them into the frame with `unshard(gbuf)`.
+    One dist.gather: on RCCL a group of point-to-point transfers into rank 0 over xGMI (each rank
+    sends its 1/N of the frame once, N - 1 shards arrive), not an all-gather that would hand every
+    rank the whole frame.  Returns unshard's result on rank 0, None elsewhere."""
     import torch.distributed as dist
 
     if world == 1:
         return unshard(accum) if rank == 0 else None
-    if dist.get_backend() == "gloo":
-        stride = accum.shape[0]
-        dist.all_gather([gbuf[i * stride:(i + 1) * stride] for i in range(world)], accum)
-    else:
-        dist.all_gather_into_tensor(gbuf, accum)
+    stride = accum.shape[0]
+    parts = [gbuf[i * stride:(i + 1) * stride] for i in range(world)] if rank == 0 else None
+    dist.gather(accum, gather_list=parts, dst=0)
     return unshard(gbuf) if rank == 0 else None

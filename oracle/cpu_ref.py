@@ -81,13 +81,15 @@ class RefOctree(C.Structure):
 _lib = None
 
 
-def load() -> C.CDLL:
+def load(path: str | Path | None = None) -> C.CDLL:
+    """Bind the oracle library (the portable x86-64-v2 build; bench.py's CPU baseline passes its
+    -O3 -march=native build of the same source, which then serves every later call)."""
     global _lib
-    if _lib is not None:
+    if _lib is not None and path is None:
         return _lib
-    if not LIB_PATH.exists():
+    if path is None and not LIB_PATH.exists():
         build()
-    lib = C.CDLL(str(LIB_PATH))
+    lib = C.CDLL(str(path or LIB_PATH))
     f, u32, vp = C.c_float, C.c_uint32, C.c_void_p
     for name in ("ref_math_sin", "ref_math_cos", "ref_math_asin", "ref_math_acos"):
         getattr(lib, name).restype = f

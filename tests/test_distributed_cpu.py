@@ -39,7 +39,7 @@ def _worker(rank, world, port, W, H, q):
         stride = D.shard_stride(W, H, world)
         assert _lib.load().octpt_shard_pixels(W, H, rank, world) == D.shard_tile_count(W, H, rank, world) * 64
         shard = torch.from_numpy(D.extract_shard(frame, W, H, rank, world, stride))
-        gbuf = torch.zeros((world * stride, 4), dtype=torch.float32)
+        gbuf = torch.zeros((world * stride, 4), dtype=torch.float32) if rank == 0 else None
         out = D.gather_frame(shard, gbuf, W, H, rank, world,
                              lambda g: D.unshard_host(g.numpy(), W, H, world, stride))
         if rank == 0:

@@ -1,0 +1,35 @@
+"""bench.py's N-rank path on one GPU: `--gpus 2` spawns two ranks itself, each renders
+its 8x8-tile shard through liboctpt on the GPU, the shards are gathered to rank 0 (gloo, host-staged:
+two ranks share this box's one GPU, which RCCL does not allow) and unsharded by the kernel.  The
+gathered frame must equal the one-rank frame bit for bit and the JSON line must report n_gpus 2."""
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _bench(tmp_path, n, extra=()):
+    out = tmp_path / f"frame{n}.npy"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--config", "C2", "--spp", "2", "--steps", "1",
+           "--warmup", "0", "--no-cpu-baseline", "--dump-frame", str(out), *extra]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    return line, np.load(out)
+
+
+def test_two_ranks_gather_equals_one(tmp_path):
+    one, f1 = _bench(tmp_path, 1)
+    two, f2 = _bench(tmp_path, 2, ("--dist-backend", "gloo"))
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["config"]["parallelism"] == "tiles2-gloo"
+    assert f1.shape == f2.shape == (1280 * 720, 4)
+    assert np.array_equal(f1, f2)
+    # every rank's segments are counted once
+    assert one["config"]["segments_per_step"] == two["config"]["segments_per_step"]
