@@ -33,7 +33,6 @@ constexpr uint32_t kLookahead = 3;                  // host steering: iterations
 constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (57 GB of queues + path state)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
 constexpr uint32_t kDefaultRefill = 0;               // extend: idle lanes before a wave refills (0: adaptive)
-constexpr uint32_t kDefaultLeafBatch = 0;            // extend: parked lanes before a wave tests leaves (0: inline)
 
 uint32_t env_u32(const char *name, uint32_t dflt) {
     const char *v = std::getenv(name);
@@ -89,7 +88,7 @@ struct octpt_ctx {
     float build_ms = 0.0f;  // device time of the last octpt_build_octree_device
     BuildScratch build_scratch;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
-    int extend_bpc_cache[kMaxDepth + 1][3][4] = {};  // [depth][kPrims][variant]
+    int extend_bpc_cache[kMaxDepth + 1][3] = {};  // [depth][kPrims]
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
     size_t pool = 0, color_cap = 0, nee_pool = 0;  // nee_pool: slots of the sun-sampling planes (wb.pd)
@@ -98,7 +97,7 @@ struct octpt_ctx {
     void *color_alloc = nullptr;
     uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
     hipEvent_t count_ev[kLookahead + 1] = {};
-    uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill, leaf_batch = kDefaultLeafBatch;
+    uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
     uint64_t chunk_cap = kDefaultChunkPaths;  // (pixel, sample) items per chunk (OCTPT_CHUNK)
     // one asynchronous frame may be in flight; device-touching calls join it first
     octpt_frame *inflight = nullptr;
@@ -556,12 +555,12 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
     octpt_status st = ensure_wave(ctx, pool, chunk_max, ctx->S.sun.sun_sampling != 0);
     if (st != OCTPT_OK) return st;
-    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)][(ctx->leaf_batch & kLeafSpec) ? 3 : ctx->leaf_batch == kLeafSplit ? 2 : (ctx->leaf_batch ? 1 : 0)];
-    if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S, ctx->leaf_batch);
+    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)];
+    if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S);
     const int grid_extend = ctx->num_cu * bpc;
     if (std::getenv("OCTPT_DEBUG"))
-        std::fprintf(stderr, "octpt: extend %d blocks/CU x %d CUs (depth %u, cuboids %u, variant %u), pool %zu\n", bpc,
-                     ctx->num_cu, ctx->S.depth, ctx->S.has_cuboids, ctx->leaf_batch, pool);
+        std::fprintf(stderr, "octpt: extend %d blocks/CU x %d CUs (depth %u, cuboids %u, models %u), pool %zu\n", bpc,
+                     ctx->num_cu, ctx->S.depth, ctx->S.has_cuboids, ctx->S.has_models, pool);
     // shade maps waves to queue segments: a multiple of kSegs waves (kSegs / 4 blocks)
     const int seg_blocks = (int)(kSegs * 64u / kBlock);
     const int shade_bpc = (int)std::min<uint32_t>(env_u32("OCTPT_SHADE_BPC", 4u), 8u);  // blocks per CU
@@ -591,7 +590,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             const uint32_t q = it & 1u;
             EventPair ev{};
             if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
-            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, ctx->leaf_batch, grid_extend, ctx->d_stats, s));
+            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, grid_extend, ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
             if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
             HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, grid_shade, ctx->d_stats, s));
@@ -805,13 +804,6 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->refill = (refill_env && *refill_env)
                       ? std::max<uint32_t>(std::min<uint32_t>(env_u32("OCTPT_REFILL", 16u), 64u), 1u)
                       : kDefaultRefill;
-    ctx->leaf_batch = std::min<uint32_t>(env_u32("OCTPT_LEAF_BATCH", kDefaultLeafBatch), 64u);
-    if (const char *m = std::getenv("OCTPT_EXTEND")) {  // extend variant: "split" = wave-specialised
-        if (std::string(m) == "split") ctx->leaf_batch = kLeafSplit;
-        if (std::string(m) == "spec")
-            ctx->leaf_batch = kLeafSpec | std::min<uint32_t>(env_u32("OCTPT_SPEC_BATCH", 16), 64u) |
-                              (std::min<uint32_t>(env_u32("OCTPT_SPEC_STALL", 8), 64u) << 8);
-    }
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);
@@ -1309,6 +1301,17 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     unsigned long long v[kStatCount] = {0};
     for (uint32_t r = 0; r < kSegs; ++r)
         for (uint32_t i = 0; i < kStatCount; ++i) v[i] += rows[r * kStatRow + i];
+    if (std::getenv("OCTPT_PROFILE_LANES")) {  // diagnostic builds (-DOCTPT_PROFILE_LANES) fill words 8..16
+        static const char *names[9] = {"iters", "active", "leaf_it", "leaf_ln", "pop_it", "pop_ln", "push_it",
+                                       "desc_ln", "exact"};
+        std::fprintf(stderr, "octpt lanes:");
+        for (uint32_t i = 0; i < 9; ++i) {
+            unsigned long long x = 0;
+            for (uint32_t r = 0; r < kSegs; ++r) x += rows[r * kStatRow + 8 + i];
+            std::fprintf(stderr, " %s=%llu", names[i], x);
+        }
+        std::fprintf(stderr, "\n");
+    }
     out->paths = v[kStatPaths];
     out->segments = v[kStatSegments];
     out->esvo_steps = v[kStatSteps];

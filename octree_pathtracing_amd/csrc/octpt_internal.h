@@ -182,12 +182,6 @@ enum StatIndex {
 constexpr uint32_t kStatRow = 32;
 constexpr uint32_t kStatWords = kSegs * kStatRow;
 
-// extend variants (launch_wf_extend's leaf_batch): 0 leaf tests inline, 1..64 wave-local deferral,
-// kLeafSplit the wave-specialised kernel (3 traversal waves + 1 leaf-test wave per block)
-constexpr uint32_t kLeafSplit = 0xFFFFu;
-// speculative extend (wf_extend_spec_kernel): kLeafSpec | batch | stall << 8
-constexpr uint32_t kLeafSpec = 0x10000u;
-
 // kernel launchers (octpt_kernels.hip)
 hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
                           uint32_t *segcount, unsigned long long *stats, hipStream_t stream);
@@ -196,13 +190,13 @@ hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender 
                          hipStream_t stream);
 hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t n_seed,
                           uint32_t chunk_items, unsigned long long *stats, hipStream_t stream);
-hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill,
-                            uint32_t leaf_batch, int grid, unsigned long long *stats, hipStream_t stream);
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
+                            unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
                            uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,
                              uint32_t *segcount, hipStream_t stream);
-int extend_blocks_per_cu(const DevScene &S, uint32_t leaf_batch);
+int extend_blocks_per_cu(const DevScene &S);
 hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t *last_prim,
                             const float *last_normal, uint32_t n, float *t, uint32_t *prim, float *normal,
                             uint32_t *steps, hipStream_t stream);

@@ -218,12 +218,25 @@ struct Esvo {
     v3 t_coef, t_bias, pos;
     float t_min, t_max, h, scale_exp2;
     uint32_t parent, pmask, idx, mirror, iter;  // scale = exponent of scale_exp2 + OCTREE_MAX_SCALE - 127
-    bool resume;  // re-entering a step whose deferred leaf test missed: go straight to advance
 };
 
 struct Counters {
     uint32_t paths, segs, steps, sph, cub, shade, tex;
+#ifdef OCTPT_PROFILE_LANES  // diagnostic builds: per-wave lane occupancy of extend's step (stat words 8..)
+    uint32_t p_iters, p_active, p_leaf_it, p_leaf_ln, p_pop_it, p_pop_ln, p_push_it, p_desc_ln, p_exact;
+#endif
 };
+
+#ifdef OCTPT_PROFILE_LANES
+// counted once per wave (by its first active lane): whether any lane has `cond`, and how many
+__device__ __forceinline__ void prof_wave(uint32_t &it, uint32_t &ln, bool cond) {
+    const uint64_t m = __ballot(cond), e = __ballot(true);
+    if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)e) - 1u) {
+        it += m != 0ull ? 1u : 0u;
+        ln += (uint32_t)__popcll(m);
+    }
+}
+#endif
 
 __device__ __forceinline__ uint32_t f2u32_sat(float f) {
     if (!(f > 0.0f)) return 0u;
@@ -295,6 +308,63 @@ __device__ __forceinline__ bool sphere_test(float4 sp, const TraceRay &r, bool s
         ok = near_ok || h.t > RAY_EPSILON;
     }
     return ok;
+}
+
+// The root a sphere hit was accepted with, recomputed exactly (sphere_test's operations for that
+// root): the wavefront extend decides sphere hits with sphere_decide's error-bounded estimate and
+// its hit records carry that root (inside flag), not t; shade recomputes t here.
+__device__ __forceinline__ float sphere_root(float4 sp, v3 o, v3 d, bool far) {
+    const v3 oc = vsub(V(sp.x, sp.y, sp.z), o);
+    const float a = vdot(d, d);
+    const float hh = vdot(d, oc);
+    const float cc = vdot(oc, oc) - sp.w * sp.w;
+    const float sq = sqrtf(hh * hh - a * cc);
+    return far ? (hh + sq) / a : (hh - sq) / a;
+}
+
+enum : int { kDecideMiss = 0, kDecideHit = 1, kDecideExact = 2 };
+
+// sphere_test + the leaf's acceptance (t <= t_accept, C1) decided from an estimate: the hardware
+// square root and reciprocal (v_sqrt_f32 / v_rcp_f32, 1 ulp each) instead of the correctly rounded
+// expansions (~40 instructions, most of a leaf visit).  Every decision of the exact test -- disc >= 0,
+// near root > EPSILON, far root > EPSILON, t <= t_accept -- compares a root against a threshold; the
+// estimate differs from the exact root by less than m/2 with
+//   m = (|hh| + sq) / a * 2^-19
+// (|hh +- sq| <= |hh| + sq; sqrt 1.5 ulp, two roundings of the sum, reciprocal and product ~3 ulp,
+// i.e. < 2^-20.2 (|hh| + sq) / a, kept with a factor 2 of slack), so a root farther than m from a
+// threshold decides exactly as the exact test would.  Closer than m, or a sub-normal-range disc or a
+// far from unit a, returns kDecideExact and the caller runs sphere_test.  disc, hh and a are the exact
+// test's own values (same operations).  On kDecideHit, h.f = the root (inside flag); h.t is the
+// estimate, never used as the hit's t (shade recomputes it with sphere_root).
+__device__ __forceinline__ int sphere_decide(float4 sp, const TraceRay &r, bool self_prim, float t_accept, PrimHit &h) {
+    const v3 oc = vsub(V(sp.x, sp.y, sp.z), r.o);
+    const float a = vdot(r.d, r.d);
+    const float hh = vdot(r.d, oc);
+    const float cc = vdot(oc, oc) - sp.w * sp.w;
+    const float disc = hh * hh - a * cc;
+    if (!(disc >= 0.0f) || (self_prim && !r.self_inward)) return kDecideMiss;
+    if (disc < 0x1p-100f || !(a > 0x1p-8f && a < 0x1p8f)) return kDecideExact;
+    const float sq = __builtin_amdgcn_sqrtf(disc);
+    const float ra = __builtin_amdgcn_rcpf(a);
+    const float m = ((fabsf(hh) + sq) * ra) * 0x1p-19f;
+    bool far = self_prim;
+    float t = 0.0f;
+    if (!self_prim) {
+        t = (hh - sq) * ra;
+        if (!(t > RAY_EPSILON + m)) {
+            if (!(t <= RAY_EPSILON - m)) return kDecideExact;
+            far = true;  // the near root is <= EPSILON exactly too: sphere_test takes the far root
+        }
+    }
+    if (far) {
+        t = (hh + sq) * ra;
+        if (!(t > RAY_EPSILON + m)) return t <= RAY_EPSILON - m ? kDecideMiss : kDecideExact;
+    }
+    if (t > t_accept + m) return kDecideMiss;
+    if (!(t <= t_accept - m)) return kDecideExact;
+    h.t = t;
+    h.f = far ? 1u : 0u;
+    return kDecideHit;
 }
 
 __device__ __forceinline__ float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6f : 1.0f / d; }
@@ -532,16 +602,9 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (upper.y > E.t_min) { E.idx ^= 2u; E.pos.y = 1.5f; }
     if (upper.z > E.t_min) { E.idx ^= 4u; E.pos.z = 1.5f; }
     E.iter = 0u;
-    E.resume = false;
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
-#ifndef OCTPT_FLAT_EXIT
-#define OCTPT_FLAT_EXIT 1
-#endif
-#ifndef OCTPT_HIT_FALLTHROUGH
-#define OCTPT_HIT_FALLTHROUGH 1
-#endif
 
 
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
@@ -582,12 +645,27 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
 // registers (70 instead of 85 VGPRs in wf_extend_kernel: 7 waves/SIMD instead of 5).
 // The first primitive is tested straight-line (leaves hold 1.02 primitives on average); the
 // rest of a multi-primitive list in a loop, keeping the closest accepted hit.
-template <int kPrims = kPrimsModels>
+// kFast (wavefront extend): a single-sphere leaf is decided by sphere_decide, falling back to the
+// exact test only when the estimate lies too close to a threshold; its hit carries the root, not t.
+template <int kPrims = kPrimsModels, bool kFast = false>
 __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt, const float4 *pre = nullptr) {
     uint32_t prim = lr.x;
     if (lr.y != 1u) prim = S.leaf_prims[lr.x];
     bool found;
+    if (kFast && lr.y == 1u && (kPrims == kPrimsSpheres || !(prim & kPrimCuboidBit))) {
+        cnt.sph++;
+        const float4 sp = (kPrims == kPrimsSpheres && pre) ? *pre : S.spheres[prim];
+        const bool self_prim = prim == r.last_prim;
+        const int d = sphere_decide(sp, r, self_prim, t_accept, best);
+#ifdef OCTPT_PROFILE_LANES
+        cnt.p_exact += d == kDecideExact ? 1u : 0u;
+#endif
+        if (__builtin_expect(d == kDecideExact, 0)) found = sphere_test(sp, r, self_prim, best) && best.t <= t_accept;
+        else found = d == kDecideHit;
+        if (found) best_prim = prim;
+        return found;
+    }
     if (kPrims == kPrimsSpheres && pre && lr.y == 1u) {
         // single-sphere leaf: its sphere arrived with the slot (leaf_sph, loaded beside node_child)
         cnt.sph++;
@@ -608,66 +686,47 @@ __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr,
     return found;
 }
 
-enum : int { kStepLeaf = 3 };
-
-// one ESVO iteration; on kStepHit (prim, h) hold the accepted primitive hit.  kDefer: a leaf is
-// not tested here -- the step returns kStepLeaf with (leaf, t_accept) and E.resume set; the caller
-// tests the leaf later (wave-batched) and, on a miss, calls esvo_step again, which then performs
-// the same iteration's advance without counting the iteration twice (octree_traversal.rs:142-260).
-template <bool kDefer, int kPrims = kPrimsModels, uint32_t kS = kBlock>
+// one ESVO iteration (octree_traversal.rs:127-300); on kStepHit (prim, h) hold the accepted
+// primitive hit.  The step-limit / max_dst miss is taken at the end: a lane past either runs the
+// step with no memory side effects (not live) and reports the miss, so the exit costs no exec-mask
+// region.  Callers add E.iter to cnt.steps when the ray finishes.
+template <int kPrims = kPrimsModels, bool kFast = false, uint32_t kS = kBlock>
 __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk, Counters &cnt,
-                                uint32_t &prim, PrimHit &h, uint2 &leaf, float &t_accept) {
+                                uint32_t &prim, PrimHit &h) {
+    // :128-130: max_dst = 1024 * 2^-depth > 0, so the reference's `max_dst >= 0` guard always holds
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
-    const bool resume = kDefer && E.resume;
-    bool stopped = false;  // OCTPT_FLAT_EXIT: the step-limit / max_dst miss, taken at the end
-    if (!kDefer && OCTPT_FLAT_EXIT) {
-        // the lane runs the step with no memory side effects (not live) and reports the miss at
-        // the end, so the exit costs no exec-mask region
-        stopped = E.iter >= OCTREE_MAX_STEPS || (max_dst >= 0.0f && E.t_min > max_dst);
-        E.iter += stopped ? 0u : 1u;
-    } else if (!resume) {
-        // on a resumed step these were checked before the deferred leaf: iter may now equal
-        // OCTREE_MAX_STEPS, and exiting here is the same miss the reference reaches after its advance
-        if (E.iter >= OCTREE_MAX_STEPS) return kStepMiss;
-        if (max_dst >= 0.0f && E.t_min > max_dst) return kStepMiss;
-        E.iter++;  // callers add E.iter to cnt.steps when the ray finishes
-    }
-    if (kDefer) E.resume = false;
+    const bool stopped = (E.iter >= OCTREE_MAX_STEPS) | (E.t_min > max_dst);
+    E.iter += stopped ? 0u : 1u;
     const v3 t_corner = vsub(vmul(E.pos, E.t_coef), E.t_bias);
     const float tc_max = tmin3(t_corner);
     const uint32_t cidx = E.idx ^ E.mirror;
-    const bool present = (E.pmask >> cidx) & 1u;
-    const bool is_leaf = (E.pmask >> (cidx + 8u)) & 1u;
+    // the child's two mask bits in one word: 0x101 leaf, 0x001 octant (bit 0 present, bit 8 leaf)
+    const uint32_t kind = (E.pmask >> cidx) & 0x101u;
     // :142-244.  Leaf (t_min >= 0) and descend (t_min <= min(t_max, tc_max)) lanes share one slot
     // load instruction: on CDNA4 a scattered load costs the vector-memory pipe per instruction.
-    const bool live = present && E.t_min <= E.t_max && !stopped;
+    // (t_min <= tv_max implies the reference's t_min <= t_max for the descend.)
     const float tv_max = tmn(E.t_max, tc_max);
-    const bool take_leaf = live && is_leaf && E.t_min >= 0.0f && !resume;
-    const bool descend = live && !is_leaf && E.t_min <= tv_max;
+    const bool take_leaf = (kind == 0x101u) & !stopped & (E.t_min <= E.t_max) & (E.t_min >= 0.0f);
+    const bool descend = (kind == 0x001u) & !stopped & (E.t_min <= tv_max);
     uint2 slot = make_uint2(0u, 0u);
     const uint32_t sidx = E.parent + __popc(E.pmask & ((1u << cidx) - 1u));
     if (take_leaf || descend) slot = S.node_child[sidx];
     // sphere-only scenes: a leaf's first sphere is loaded beside its slot (no dependent second load)
     float4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (kPrims == kPrimsSpheres && take_leaf) lsph = S.leaf_sph[sidx];
+#ifdef OCTPT_PROFILE_LANES
+    prof_wave(cnt.p_leaf_it, cnt.p_leaf_ln, take_leaf);
+    prof_wave(cnt.p_push_it, cnt.p_desc_ln, descend);
+#endif
     bool leaf_hit = false;
     if (take_leaf) {
         // x / 2^-depth == x * 2^depth exactly (the oracle divides)
         const float cell_w = E.scale_exp2 * S.inv_octree_scale;
-        t_accept = tc_max * S.inv_octree_scale + CELL_TOL * cell_w;
-        if (kDefer) {
-            leaf = slot;
-            E.resume = true;
-            return kStepLeaf;
-        }
-#if OCTPT_HIT_FALLTHROUGH
+        const float t_accept = tc_max * S.inv_octree_scale + CELL_TOL * cell_w;
         // a hit lane runs the advance below too (its state is discarded): the descend / advance
         // block then needs no exec-mask region of its own
-        leaf_hit = leaf_test<kPrims>(S, ray, slot, t_accept, prim, h, cnt, kPrims == kPrimsSpheres ? &lsph : nullptr);
-#else
-        if (leaf_test<kPrims>(S, ray, slot, t_accept, prim, h, cnt, kPrims == kPrimsSpheres ? &lsph : nullptr))
-            return kStepHit;
-#endif
+        leaf_hit = leaf_test<kPrims, kFast>(S, ray, slot, t_accept, prim, h, cnt,
+                                            kPrims == kPrimsSpheres ? &lsph : nullptr);
     }
     // Descend (:216-244) and advance (:249-260) as one select-based update: every lane computes
     // X = t_coef * f + t_corner with f = half for descend (X = t_center) and f = 0 otherwise
@@ -700,17 +759,22 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     E.t_min = descend ? E.t_min : tc_max;
     E.idx = descend ? step_mask : (E.idx ^ step_mask);
     bool escaped = false;
+#ifdef OCTPT_PROFILE_LANES
+    prof_wave(cnt.p_pop_it, cnt.p_pop_ln, !descend && (E.idx & step_mask) != 0u);
+#endif
     if (!descend && (E.idx & step_mask) != 0u) {  // pop (:262-299)
         // the three axes' differing bits are selected, not branched on (no exec-mask region)
         const uint32_t dx = __float_as_uint(E.pos.x) ^ __float_as_uint(E.pos.x + E.scale_exp2);
         const uint32_t dy = __float_as_uint(E.pos.y) ^ __float_as_uint(E.pos.y + E.scale_exp2);
         const uint32_t dz = __float_as_uint(E.pos.z) ^ __float_as_uint(E.pos.z + E.scale_exp2);
         const uint32_t diff = ((step_mask & 1u) ? dx : 0u) | ((step_mask & 2u) ? dy : 0u) | ((step_mask & 4u) ? dz : 0u);
-        const uint32_t scale_raw = diff ? 31u - (uint32_t)__clz(diff) : 0xFFFFFFFFu;
+        // diff != 0: a stepped axis moved by scale_exp2, so its pos differs from pos + scale_exp2
+        // (the reference's diff == 0 case, util.rs:121-133, cannot arise here)
+        const uint32_t scale_raw = 31u - (uint32_t)__clz(diff);
         // escaping the root is a miss (:281-283); its lane finishes the block on a clamped scale
         // and reports the miss at the end, so the pop stays one branch level
         escaped = scale_raw >= OCTREE_MAX_SCALE;
-        const uint32_t scale = escaped ? OCTREE_MAX_SCALE - 1u : scale_raw;
+        const uint32_t scale = min(scale_raw, OCTREE_MAX_SCALE - 1u);
         E.scale_exp2 = __uint_as_float((scale - OCTREE_MAX_SCALE + 127u) << 23);
         // a pop rises above the level it advanced at (the step's own bit, 2^(s-23) in pos's
         // mantissa, always differs, and the pop condition means a higher one does), so
@@ -721,14 +785,15 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         E.parent = e.x;
         E.pmask = em;
         E.t_max = __uint_as_float(e.y);
-        const uint32_t shx = __float_as_uint(E.pos.x) >> scale;
-        const uint32_t shy = __float_as_uint(E.pos.y) >> scale;
-        const uint32_t shz = __float_as_uint(E.pos.z) >> scale;
-        E.pos = V(__uint_as_float(shx << scale), __uint_as_float(shy << scale), __uint_as_float(shz << scale));
-        E.idx = (shx & 1u) | ((shy & 1u) << 1) | ((shz & 1u) << 2);
+        // pos truncated to the popped scale; idx = pos bits at that scale
+        const uint32_t keep = 0xFFFFFFFFu << scale;
+        const uint32_t px = __float_as_uint(E.pos.x) & keep, py = __float_as_uint(E.pos.y) & keep,
+                       pz = __float_as_uint(E.pos.z) & keep;
+        E.pos = V(__uint_as_float(px), __uint_as_float(py), __uint_as_float(pz));
+        E.idx = ((px >> scale) & 1u) | (((py >> scale) & 1u) << 1) | (((pz >> scale) & 1u) << 2);
         E.h = 0.0f;
     }
-    return leaf_hit ? kStepHit : ((escaped || stopped) ? kStepMiss : kStepContinue);
+    return leaf_hit ? kStepHit : ((escaped | stopped) ? kStepMiss : kStepContinue);
 }
 
 // ---------------------------------------------------------------------------
@@ -1114,9 +1179,17 @@ __device__ inline void flush_counters(const Counters &cnt, unsigned long long *s
 #ifdef OCTPT_NO_STATS  // A/B builds only: every counter update becomes dead code
     return;
 #endif
-    const uint32_t vals[kStatCount] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};
+#ifdef OCTPT_PROFILE_LANES
+    constexpr int kN = kStatCount + 1 + 9;
+    const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex, 0u,
+                               cnt.p_iters, cnt.p_active, cnt.p_leaf_it, cnt.p_leaf_ln, cnt.p_pop_it, cnt.p_pop_ln,
+                               cnt.p_push_it, cnt.p_desc_ln, cnt.p_exact};
+#else
+    constexpr int kN = kStatCount;
+    const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};
+#endif
 #pragma unroll
-    for (int i = 0; i < kStatCount; ++i) {
+    for (int i = 0; i < kN; ++i) {
         const unsigned long long s = wave_sum(vals[i]);
         if ((threadIdx.x & 63u) == 0u && s) atomicAdd(&stats[(blockIdx.x % kSegs) * kStatRow + i], s);
     }
@@ -1202,9 +1275,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             }
             first = false;
             if (state == ST_TRAV) {
-                uint2 lf;
-                float ta;
-                const int rs = esvo_step<false>(S, tr, E, stk, cnt, hprim, hh, lf, ta);
+                const int rs = esvo_step(S, tr, E, stk, cnt, hprim, hh);
                 if (rs == kStepHit) state = ST_HIT;
                 else if (rs == kStepMiss) state = ST_MISS;
                 if (rs != kStepContinue) cnt.steps += E.iter;
@@ -1287,11 +1358,9 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
             esvo_begin(S, tr, E, stk);
             uint32_t prim = kPrimNone;
             PrimHit h;
-            uint2 lf;
-            float ta;
             int rs;
             do {
-                rs = esvo_step<false, kPrims>(S, tr, E, stk, cnt, prim, h, lf, ta);
+                rs = esvo_step<kPrims>(S, tr, E, stk, cnt, prim, h);
             } while (rs == kStepContinue);
             cnt.steps += E.iter;
             if (rs != kStepHit) break;  // a miss leaves the last hit record in place
@@ -1475,9 +1544,6 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #ifndef OCTPT_EXTEND_WAVES
 #define OCTPT_EXTEND_WAVES 1
 #endif
-#ifndef OCTPT_EXTEND_NESTED
-#define OCTPT_EXTEND_NESTED 1
-#endif
 // minimum waves per SIMD a wf_extend_kernel instance is compiled for (register budget)
 // (measured at 64 spp against the unconstrained allocation: the few spilled dwords sit in cold
 // code, the extra waves hide the slot loads' latency)
@@ -1496,9 +1562,9 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 constexpr uint32_t kClaim = 64u;
 // refill == 0 (adaptive): rays shorter than this many ESVO steps on average refill 32 at a time
 constexpr uint32_t kShortRaySteps = 56u;
-template <bool kDefer, int kPrims>
+template <int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
-                                                           uint32_t leaf_batch, unsigned long long *__restrict__ stats) {
+                                                           unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
     const Stack stk = stack_of(lds_stack, S.depth);
     const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
@@ -1512,12 +1578,10 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
     bool rays_left = true;  // wave-uniform: some segment may still hold unclaimed rays
     uint32_t segs_w = 0u;   // segments started by this wave
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    bool active = false, pend = false;
+    bool active = false;
     uint32_t pos = 0u;
     TraceRay tr;
     Esvo E;
-    uint2 leaf = make_uint2(0u, 0u);
-    float t_accept = 0.0f;
     bool more = true;
     // chunked claims: the wave owns [c_next, c_end) of segment seg and holds one further claim in
     // flight (lane 0's atomic result, read only when the owned chunk runs out), so a refill hands
@@ -1574,375 +1638,27 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 thr = __popcll(__ballot(short_rays)) > 32 ? 32u : 16u;
             }
         }
-#if OCTPT_EXTEND_NESTED
-        if constexpr (!kDefer) {
-            // inner loop: step until `refill` lanes are idle (every lane, once no ray is left); its
-            // only per-iteration bookkeeping is one ballot, a popcount and a scalar branch
-            const uint32_t stop_at = __builtin_amdgcn_readfirstlane(rays_left ? thr : 64u);  // keeps the loop scalar
-            if ((uint32_t)__popcll(__ballot(!active)) < stop_at) do {
-#ifdef OCTPT_INJECT_SALU
-                {
-                    uint32_t sd = __builtin_amdgcn_readfirstlane(pos);
-#pragma unroll
-                    for (int k = 0; k < OCTPT_INJECT_SALU; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sd));
-                    if (sd == 0xDEADBEEFu) segs_w++;
-                }
+        // inner loop: step until `thr` lanes are idle (every lane, once no ray is left); its only
+        // per-iteration bookkeeping is one ballot, a popcount and a scalar branch
+        const uint32_t stop_at = __builtin_amdgcn_readfirstlane(rays_left ? thr : 64u);  // keeps the loop scalar
+        if ((uint32_t)__popcll(__ballot(!active)) < stop_at) do {
+#ifdef OCTPT_PROFILE_LANES
+            prof_wave(cnt.p_iters, cnt.p_active, active);
 #endif
-                if (active) {
-                    uint32_t prim = kPrimNone;
-                    PrimHit h;
-                    const int rs = esvo_step<false, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
-                    if (rs != kStepContinue) {
-                        B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
-                        cnt.steps += E.iter;
-                        active = false;
-                    }
-                }
-            } while ((uint32_t)__popcll(__ballot(!active)) < stop_at);  // at the bottom: no phi copies
-            more = rays_left;  // wave-uniform; every lane is idle when it is false
-            continue;
-        }
-#endif
-        const uint64_t am = __ballot(active);
-        // the loop ends after a pass in which no lane was active and no ray was left (with am == 0
-        // the step below does nothing).  Testing it at the bottom, made uniform by readfirstlane,
-        // keeps this a scalar-branch loop instead of an exec-mask loop.
-        more = __builtin_amdgcn_readfirstlane((am != 0ull || rays_left) ? 1u : 0u) != 0u;
-#ifdef OCTPT_INJECT_SALU  // cost experiment: OCTPT_INJECT_SALU extra scalar ALU instructions per iteration
-        {
-            uint32_t sd = __builtin_amdgcn_readfirstlane(pos);
-#pragma unroll
-            for (int k = 0; k < OCTPT_INJECT_SALU; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sd));
-            if (sd == 0xDEADBEEFu) segs_w++;
-        }
-#endif
-#ifdef OCTPT_INJECT_VALU  // cost experiment: OCTPT_INJECT_VALU extra vector ALU instructions per iteration
-        {
-            uint32_t vd = pos;
-#pragma unroll
-            for (int k = 0; k < OCTPT_INJECT_VALU; ++k) asm volatile("v_add_u32 %0, %0, 1" : "+v"(vd));
-            if (vd == 0xDEADBEEFu) cnt.tex++;
-        }
-#endif
-        // deferred leaf tests [kStepLeaf]: run once leaf_batch lanes wait, or every active lane does
-        const uint64_t pm = kDefer ? __ballot(pend) : 0ull;
-        if (pm != 0ull && ((uint32_t)__popcll(pm) >= leaf_batch || pm == am)) {
-            if (pend) {
-                pend = false;
+            if (active) {
                 uint32_t prim = kPrimNone;
                 PrimHit h;
-                if (leaf_test<kPrims>(S, tr, leaf, t_accept, prim, h, cnt)) {
-                    B.hit[pos] = hit_record(prim, h);
+                const int rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
+                if (rs != kStepContinue) {
+                    B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
                     cnt.steps += E.iter;
                     active = false;
                 }
             }
-        }
-        if (active && !pend) {
-            uint32_t prim = kPrimNone;
-            PrimHit h;
-            const int rs = esvo_step<kDefer, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
-            if (rs == kStepLeaf) {
-                pend = true;
-            } else if (rs != kStepContinue) {
-                B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
-                cnt.steps += E.iter;
-                active = false;
-            }
-        }
+        } while ((uint32_t)__popcll(__ballot(!active)) < stop_at);  // at the bottom: no phi copies
+        more = rays_left;  // wave-uniform; every lane is idle when it is false
     } while (more);
     cnt.segs = (threadIdx.x & 63u) == 0u ? segs_w : 0u;  // flush_counters sums over the wave's lanes
-    flush_counters(cnt, stats);
-}
-
-// ---------------------------------------------------------------------------
-// Speculative extend (OCTPT_EXTEND=spec): a lane reaching a leaf posts the leaf test as its pending
-// job and keeps traversing as if the leaf missed (the leaf-miss advance of esvo_step's resume
-// path).  The wave runs its pending leaf tests together, once `batch` lanes hold one, `stall`
-// lanes are stalled, or no lane can step.  A hit of the job is the ray's answer (leaves are
-// visited front to back, so the speculative steps taken since are discarded, and so are their
-// counts); a miss means the speculation was the traversal.  A lane reaching a second leaf, or
-// the end of its ray, while its job is pending waits for the batch.  Results and counters equal
-// wf_extend_kernel's exactly.
-// ---------------------------------------------------------------------------
-template <int kPrims>
-__global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES) void wf_extend_spec_kernel(DevScene S, WaveBuffers B, uint32_t q,
-                                                                                uint32_t refill, uint32_t spec,
-                                                                                unsigned long long *__restrict__ stats) {
-    extern __shared__ uint2 lds_stack[];
-    const Stack stk = stack_of(lds_stack, S.depth);
-    const uint32_t batch = spec & 0xFFu, stall_max = (spec >> 8) & 0xFFu;
-    const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
-    if (blockIdx.x == 0 && threadIdx.x < kSegs) {
-        B.ctrl[ctr_count(q ^ 1u, threadIdx.x)] = 0u;
-        B.ctrl[ctr_head(q ^ 1u, threadIdx.x)] = 0u;
-    }
-    uint32_t seg = __builtin_amdgcn_readfirstlane(((blockIdx.x * kBlock + threadIdx.x) >> 6) % kSegs);
-    uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
-    bool rays_left = true;
-    uint32_t segs_w = 0u;
-    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    bool active = false;  // the lane owns a ray
-    bool job = false;     // a leaf test is pending: (jleaf, jt, jiter)
-    bool wait = false;    // stalled until the batch: a second leaf (E.resume set) or the ray's end (fin)
-    bool fin = false;
-    uint32_t pos = 0u, jiter = 0u;
-    uint2 jleaf = make_uint2(0u, 0u);
-    float jt = 0.0f;
-    TraceRay tr;
-    Esvo E;
-    uint2 leaf = make_uint2(0u, 0u);
-    float t_accept = 0.0f;
-    for (;;) {
-        const bool idle = !active;
-        const uint64_t im = __ballot(idle);
-        if (rays_left && im != 0ull && ((uint32_t)__popcll(im) >= refill || ~im == 0ull)) {
-            const uint32_t my = wave_ticket(B.ctrl + ctr_head(q, seg), idle);
-            bool dry = false;
-            if (idle) {
-                if (my < seg_n) {
-                    pos = seg * B.seg_cap + my;
-                    const float4 r0 = ray0[pos], r1 = ray1[pos];
-                    tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
-                                        (__float_as_uint(r1.w) >> 31) != 0u);
-                    esvo_begin(S, tr, E, stk);
-                    active = true;
-                } else {
-                    dry = true;
-                }
-            }
-            segs_w += (uint32_t)__popcll(__ballot(idle && !dry));
-            if (__ballot(dry) != 0ull) {
-                const uint32_t j = threadIdx.x & 63u;
-                const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, j)) < B.ctrl[ctr_count(q, j)]);
-                rays_left = m != 0ull;
-                if (rays_left) {
-                    seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
-                    seg_n = B.ctrl[ctr_count(q, seg)];
-                }
-            }
-        }
-        const uint64_t am = __ballot(active);
-        if (am == 0ull && !rays_left) break;
-        const uint64_t jm = __ballot(job);
-        const uint64_t sm = __ballot(active && !wait);
-        if (jm != 0ull &&
-            ((uint32_t)__popcll(jm) >= batch || (uint32_t)__popcll(__ballot(wait)) >= stall_max || sm == 0ull)) {
-            if (job) {
-                job = false;
-                uint32_t prim = kPrimNone;
-                PrimHit h;
-                if (leaf_test<kPrims>(S, tr, jleaf, jt, prim, h, cnt)) {
-                    B.hit[pos] = hit_record(prim, h);
-                    cnt.steps += jiter;
-                    active = false;
-                    wait = false;
-                    fin = false;
-                } else if (wait) {
-                    wait = false;
-                    if (fin) {  // the speculation ran to the ray's end: a miss
-                        fin = false;
-                        B.hit[pos] = make_uint2(kPrimNone, 0u);
-                        cnt.steps += E.iter;
-                        active = false;
-                    } else {  // the stalled second leaf becomes the job; E.resume advances past it
-                        job = true;
-                        jleaf = leaf;
-                        jt = t_accept;
-                        jiter = E.iter;
-                    }
-                }
-            }
-        }
-        if (active && !wait) {
-            uint32_t prim = kPrimNone;
-            PrimHit h;
-            const int rs = esvo_step<true, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
-            if (rs == kStepLeaf) {
-                if (!job) {
-                    job = true;
-                    jleaf = leaf;
-                    jt = t_accept;
-                    jiter = E.iter;
-                } else {
-                    wait = true;
-                }
-            } else if (rs != kStepContinue) {  // kStepMiss (leaves are tested in the batch)
-                if (job) {
-                    wait = true;
-                    fin = true;
-                } else {
-                    B.hit[pos] = make_uint2(kPrimNone, 0u);
-                    cnt.steps += E.iter;
-                    active = false;
-                }
-            }
-        }
-    }
-    cnt.segs = (threadIdx.x & 63u) == 0u ? segs_w : 0u;
-    flush_counters(cnt, stats);
-}
-
-// ---------------------------------------------------------------------------
-// Wave-specialised extend: waves 0-2 of a block traverse, wave 3 runs the leaf
-// primitive tests.  A traversal lane reaching a leaf posts (ray position, leaf slot, t_accept)
-// into its LDS job record and its wave keeps stepping the other lanes; the leaf wave gathers the
-// posted jobs of all 192 traversal lanes, tests them with the lanes of one wave, and answers.  A
-// miss resumes ESVO with the same iteration's advance (esvo_step kDefer), so traversal order,
-// counters and results are exactly those of wf_extend_kernel.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kTravLanes = 192;
-struct LeafJob {      // 32 B in LDS, one per traversal lane
-    uint32_t state;   // 0 idle, 1 posted, 2 answered
-    uint32_t pos;     // queue position of the ray
-    uint32_t lx, ly;  // leaf slot
-    float t_accept;
-    uint32_t prim;    // answer: kPrimNone = no accepted hit
-    float t;
-    uint32_t flags;   // inside | axis << 1 | neg << 3
-};
-
-__host__ __device__ __forceinline__ size_t split_stack_bytes(uint32_t depth) {
-    return ((size_t)(depth - 1u) * kTravLanes * (sizeof(uint2) + sizeof(uint16_t)) + 15u) & ~(size_t)15u;
-}
-
-template <int kPrims>
-__global__ __launch_bounds__(kBlock) void wf_extend_split_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
-                                                                 uint32_t unused, unsigned long long *__restrict__ stats) {
-    extern __shared__ uint2 lds_stack[];
-    __shared__ uint32_t live;            // traversal waves still running
-    __shared__ uint32_t worklist[64];    // leaf wave: job indices of one round
-    LeafJob *jobs = reinterpret_cast<LeafJob *>(reinterpret_cast<char *>(lds_stack) + split_stack_bytes(S.depth));
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
-    if (tid < kTravLanes) jobs[tid].state = 0u;
-    if (tid == 0u) live = kTravLanes / 64u;
-    if (blockIdx.x == 0 && tid < kSegs) {  // the other queue is refilled by this iteration's shade
-        B.ctrl[ctr_count(q ^ 1u, tid)] = 0u;
-        B.ctrl[ctr_head(q ^ 1u, tid)] = 0u;
-    }
-    __syncthreads();
-    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (tid >= kTravLanes) {
-        // ------------------------------------------------------------- leaf wave
-        for (;;) {
-            const bool p0 = __hip_atomic_load(&jobs[lane].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u;
-            const bool p1 = __hip_atomic_load(&jobs[lane + 64u].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u;
-            const bool p2 = __hip_atomic_load(&jobs[lane + 128u].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u;
-            const uint64_t m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2);
-            const uint32_t n0 = (uint32_t)__popcll(m0), n1 = (uint32_t)__popcll(m1), n2 = (uint32_t)__popcll(m2);
-            const uint32_t n = n0 + n1 + n2;
-            if (n == 0u) {
-                if (__hip_atomic_load(&live, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) break;
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            // compact the posted job indices into the work list (first 64 this round)
-            uint32_t r;
-            if (p0 && (r = lanes_below(m0)) < 64u) worklist[r] = lane;
-            if (p1 && (r = n0 + lanes_below(m1)) < 64u) worklist[r] = lane + 64u;
-            if (p2 && (r = n0 + n1 + lanes_below(m2)) < 64u) worklist[r] = lane + 128u;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < (n < 64u ? n : 64u)) {
-                const uint32_t j = worklist[lane];
-                const uint32_t pos = jobs[j].pos;
-                const uint2 slot = make_uint2(jobs[j].lx, jobs[j].ly);
-                const float t_accept = jobs[j].t_accept;
-                const float4 r0 = ray0[pos], r1 = ray1[pos];
-                const TraceRay tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
-                                                   (__float_as_uint(r1.w) >> 31) != 0u);
-                uint32_t prim = kPrimNone;
-                PrimHit h;
-                const bool found = leaf_test<kPrims>(S, tr, slot, t_accept, prim, h, cnt);
-                jobs[j].prim = found ? prim : kPrimNone;
-                jobs[j].t = h.t;
-                jobs[j].flags = h.f & 15u;
-                __hip_atomic_store(&jobs[j].state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            __builtin_amdgcn_wave_barrier();  // the work list is rewritten next round
-        }
-    } else {
-        // ------------------------------------------------------------- traversal waves
-        const StackT<kTravLanes> stk = stack_of<kTravLanes>(lds_stack, S.depth);
-        uint32_t seg = __builtin_amdgcn_readfirstlane((blockIdx.x * (kTravLanes / 64u) + (tid >> 6)) % kSegs);
-        uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
-        bool rays_left = true;
-        uint32_t segs_w = 0u;
-        bool active = false, pend = false;
-        uint32_t pos = 0u;
-        TraceRay tr;
-        Esvo E;
-        uint2 leaf = make_uint2(0u, 0u);
-        float t_accept = 0.0f;
-        for (;;) {
-            const bool idle = !active;
-            const uint64_t im = __ballot(idle);
-            if (rays_left && im != 0ull && ((uint32_t)__popcll(im) >= refill || ~im == 0ull)) {
-                const uint32_t my = wave_ticket(B.ctrl + ctr_head(q, seg), idle);
-                bool dry = false;
-                if (idle) {
-                    if (my < seg_n) {
-                        pos = seg * B.seg_cap + my;
-                        const float4 r0 = ray0[pos], r1 = ray1[pos];
-                        tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
-                                            (__float_as_uint(r1.w) >> 31) != 0u);
-                        esvo_begin(S, tr, E, stk);
-                        active = true;
-                    } else {
-                        dry = true;
-                    }
-                }
-                segs_w += (uint32_t)__popcll(__ballot(idle && !dry));
-                if (__ballot(dry) != 0ull) {
-                    const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, lane)) < B.ctrl[ctr_count(q, lane)]);
-                    rays_left = m != 0ull;
-                    if (rays_left) {
-                        seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
-                        seg_n = B.ctrl[ctr_count(q, seg)];
-                    }
-                }
-            }
-            const uint64_t am = __ballot(active);
-            if (am == 0ull && !rays_left) break;
-            if (pend) {  // answered leaf test?
-                if (__hip_atomic_load(&jobs[tid].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
-                    pend = false;
-                    const uint32_t prim = jobs[tid].prim;
-                    const float t = jobs[tid].t;
-                    const uint32_t flags = jobs[tid].flags;
-                    jobs[tid].state = 0u;
-                    if (prim != kPrimNone) {
-                        B.hit[pos] = make_uint2((prim & kPrimCuboidBit) | (flags << 27) | (prim & kPrimIndexMask),
-                                                __float_as_uint(t));
-                        cnt.steps += E.iter;
-                        active = false;
-                    }
-                }
-            }
-            if (active && !pend) {
-                uint32_t prim = kPrimNone;
-                PrimHit h;
-                const int rs = esvo_step<true, kPrims>(S, tr, E, stk, cnt, prim, h, leaf, t_accept);
-                if (rs == kStepLeaf) {
-                    jobs[tid].pos = pos;
-                    jobs[tid].lx = leaf.x;
-                    jobs[tid].ly = leaf.y;
-                    jobs[tid].t_accept = t_accept;
-                    __hip_atomic_store(&jobs[tid].state, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    pend = true;
-                } else if (rs != kStepContinue) {  // kStepMiss (hits come from the leaf wave)
-                    B.hit[pos] = make_uint2(kPrimNone, 0u);
-                    cnt.steps += E.iter;
-                    active = false;
-                }
-            }
-            if (__ballot(active && !pend) == 0ull && __ballot(pend) != 0ull) __builtin_amdgcn_s_sleep(1);
-        }
-        cnt.segs = lane == 0u ? segs_w : 0u;
-        if (lane == 0u) __hip_atomic_fetch_add(&live, (uint32_t)-1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
     flush_counters(cnt, stats);
 }
 
@@ -2005,6 +1721,8 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
                 const uint32_t flags = (hr.x >> 27) & 15u;
                 h.t = __uint_as_float(hr.y);
                 h.f = flags;
+                // a sphere hit record carries its root, decided by extend's estimate: t exactly
+                if (!(hr.x & kPrimCuboidBit)) h.t = sphere_root(S.spheres[hr.x & kPrimIndexMask], ps.o, ps.d, flags & 1u);
                 ps.n = V(0.0f, 0.0f, 0.0f);
                 commit_hit(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
             }
@@ -2100,9 +1818,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
     PrimHit h;
     int rs;
     do {
-        uint2 lf;
-        float ta;
-        rs = esvo_step<false>(S, tr, E, stk, cnt, prim, h, lf, ta);
+        rs = esvo_step(S, tr, E, stk, cnt, prim, h);
     } while (rs == kStepContinue);
     if (rs == kStepHit) {
         commit_hit(S, ps, prim, h, cnt);
@@ -2155,35 +1871,17 @@ int render_blocks_per_cu(uint32_t depth) {
     return blocks > 0 ? blocks : 1;
 }
 
-// the extend instance a scene / setting launches (sphere-only scenes: no slab test).
-// leaf_batch: 0 inline leaf tests, 1..64 wave-local deferral, kLeafSplit the wave-specialised kernel
-static const void *extend_instance(const DevScene &S, uint32_t leaf_batch) {
-    if (leaf_batch & kLeafSpec)
-        return S.has_models ? reinterpret_cast<const void *>(wf_extend_spec_kernel<kPrimsModels>)
-               : S.has_cuboids ? reinterpret_cast<const void *>(wf_extend_spec_kernel<kPrimsBoxes>)
-                               : reinterpret_cast<const void *>(wf_extend_spec_kernel<kPrimsSpheres>);
-    if (leaf_batch == kLeafSplit)
-        return S.has_cuboids ? reinterpret_cast<const void *>(wf_extend_split_kernel<kPrimsModels>)
-                             : reinterpret_cast<const void *>(wf_extend_split_kernel<kPrimsSpheres>);
-    if (S.has_models)
-        return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, kPrimsModels>)
-                          : reinterpret_cast<const void *>(wf_extend_kernel<false, kPrimsModels>);
-    if (S.has_cuboids)
-        return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, kPrimsBoxes>)
-                          : reinterpret_cast<const void *>(wf_extend_kernel<false, kPrimsBoxes>);
-    return leaf_batch ? reinterpret_cast<const void *>(wf_extend_kernel<true, kPrimsSpheres>)
-                      : reinterpret_cast<const void *>(wf_extend_kernel<false, kPrimsSpheres>);
+// the extend instance a scene launches: the primitive kinds it holds (sphere-only scenes: no slab test)
+static const void *extend_instance(const DevScene &S) {
+    if (S.has_models) return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsModels>);
+    if (S.has_cuboids) return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsBoxes>);
+    return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsSpheres>);
 }
 
-static size_t extend_lds_bytes(const DevScene &S, uint32_t leaf_batch) {
-    return leaf_batch == kLeafSplit ? split_stack_bytes(S.depth) + kTravLanes * sizeof(LeafJob)
-                                    : render_lds_bytes(S.depth);
-}
-
-int extend_blocks_per_cu(const DevScene &S, uint32_t leaf_batch) {
+int extend_blocks_per_cu(const DevScene &S) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S, leaf_batch), kBlock,
-                                                     extend_lds_bytes(S, leaf_batch)) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S), kBlock, render_lds_bytes(S.depth)) !=
+        hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
 }
@@ -2220,14 +1918,12 @@ hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuff
     return hipGetLastError();
 }
 
-hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill,
-                            uint32_t leaf_batch, int grid, unsigned long long *stats, hipStream_t stream) {
-    // leaf_batch 0: test leaves inside the step (no deferral).  refill 0 (adaptive) is
-    // wf_extend_kernel's; the experimental kernels take 16 for it
-    if (refill == 0u && ((leaf_batch & kLeafSpec) || leaf_batch == kLeafSplit)) refill = 16u;
-    void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &leaf_batch, &stats};
-    const hipError_t e = hipLaunchKernel(extend_instance(S, leaf_batch), dim3(grid), dim3(kBlock), args,
-                                         extend_lds_bytes(S, leaf_batch), stream);
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
+                            unsigned long long *stats, hipStream_t stream) {
+    // refill 0: the adaptive threshold
+    void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &stats};
+    const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth),
+                                         stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -1,9 +1,11 @@
 # scratch GPU command of the current step (run via gpurun from the repo root)
 set -o pipefail
-mkdir -p gpurun_out/r02
-timeout -k 10 600 python -u -m pytest tests/test_gpu_forms.py tests/test_gpu_builder.py tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread > gpurun_out/r02/new.log 2>&1 || { tail -60 gpurun_out/r02/new.log; exit 1; }
-tail -3 gpurun_out/r02/new.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r02/all.log 2>&1 || { tail -60 gpurun_out/r02/all.log; exit 1; }
-tail -3 gpurun_out/r02/all.log
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 > gpurun_out/r02/bench.json 2> gpurun_out/r02/bench.err || { tail -20 gpurun_out/r02/bench.err; exit 1; }
-cat gpurun_out/r02/bench.json
+mkdir -p gpurun_out/r02p
+R=$PWD
+echo "== lanes"; OCTPT_PROFILE_LANES=1 OCTPT_LIB=build_variants/prof/liboctpt.so timeout -k 10 300 python scripts/spp_sweep.py C3 64 --ktime 2>&1 | grep -E "spp|lanes" || exit 1
+cd /tmp && export TMPDIR=/tmp
+for lib in base cur; do
+  if [ $lib = cur ]; then unset OCTPT_LIB; else export OCTPT_LIB=$R/build_variants/base/liboctpt.so; fi
+  timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS -d $R/gpurun_out/r02p/sq_$lib -o run --output-format csv -- python3 $R/scripts/spp_sweep.py C3 64 > $R/gpurun_out/r02p/sq_$lib.log 2>&1 || exit 1
+  python3 $R/scripts/pmc_summary.py $R/gpurun_out/r02p/sq_$lib 2>&1 | grep -E "extend|==" 
+done

@@ -436,59 +436,6 @@ def test_intersect_matches_golden_rays(renderer):
     assert np.array_equal(t, g["t"]) and np.array_equal(nrm, g["normal"])
 
 
-@pytest.mark.parametrize("name,res", [("tiny", None), ("C3", (256, 144, 4)), ("C4", (96, 54, 2))])
-def test_split_extend_equals_default(torch_cuda, renderer, name, res):
-    """The wave-specialised extend kernel (OCTPT_EXTEND=split: 3 traversal waves + 1 leaf-test wave
-    per block) renders bit-identically to the default extend kernel."""
-    import os
-    from octree_pathtracing_amd import scene as S
-    from octree_pathtracing_amd.renderer import HipRenderer
-
-    sc, cam, rs = S.make_config(name)
-    if res:
-        rs.width, rs.height, rs.spp = res
-    ref = gpu_render(torch_cuda, renderer, sc, cam, rs)
-    os.environ["OCTPT_EXTEND"] = "split"
-    try:
-        r2 = HipRenderer(0)
-        out = gpu_render(torch_cuda, r2, sc, cam, rs)
-        r2.close()
-    finally:
-        del os.environ["OCTPT_EXTEND"]
-    assert np.array_equal(ref[0], out[0]) and np.array_equal(ref[1], out[1])
-    for k in ("segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events", "paths"):
-        assert ref[2][k] == out[2][k], k
-
-
-@pytest.mark.parametrize("name,res,env", [("tiny", None, {}), ("C3", (256, 144, 4), {}),
-                                          ("C4", (96, 54, 2), {"OCTPT_SPEC_BATCH": "1", "OCTPT_SPEC_STALL": "1"}),
-                                          ("blocks", None, {"OCTPT_SPEC_BATCH": "64", "OCTPT_SPEC_STALL": "64"}),
-                                          ("C5", (96, 54, 2), {})])
-def test_spec_extend_equals_default(torch_cuda, renderer, name, res, env):
-    """The speculative extend kernel (OCTPT_EXTEND=spec: leaf tests posted as jobs and batched per
-    wave while the lane keeps traversing) renders bit-identically to the default extend kernel,
-    counters included, for extreme batch / stall settings too."""
-    import os
-    from octree_pathtracing_amd import scene as S
-    from octree_pathtracing_amd.renderer import HipRenderer
-
-    sc, cam, rs = S.make_config(name)
-    if res:
-        rs.width, rs.height, rs.spp = res
-    ref = gpu_render(torch_cuda, renderer, sc, cam, rs)
-    os.environ.update({"OCTPT_EXTEND": "spec", **env})
-    try:
-        r2 = HipRenderer(0)
-        out = gpu_render(torch_cuda, r2, sc, cam, rs)
-        r2.close()
-    finally:
-        for k in ("OCTPT_EXTEND", *env):
-            del os.environ[k]
-    assert np.array_equal(ref[0], out[0]) and np.array_equal(ref[1], out[1])
-    for k in ("segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events", "paths"):
-        assert ref[2][k] == out[2][k], k
-
-
 # ---------------------------------------------------------------------------- preview mode (C16)
 @pytest.mark.parametrize("name,res", [("tiny", None), ("C1", None), ("C2", (160, 90)), ("C3", (256, 144)),
                                       ("C4", (160, 90)), ("C5", (320, 180)), ("blocks", (160, 120))])
