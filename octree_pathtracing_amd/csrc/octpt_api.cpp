@@ -1301,11 +1301,11 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     unsigned long long v[kStatCount] = {0};
     for (uint32_t r = 0; r < kSegs; ++r)
         for (uint32_t i = 0; i < kStatCount; ++i) v[i] += rows[r * kStatRow + i];
-    if (std::getenv("OCTPT_PROFILE_LANES")) {  // diagnostic builds (-DOCTPT_PROFILE_LANES) fill words 8..16
-        static const char *names[9] = {"iters", "active", "leaf_it", "leaf_ln", "pop_it", "pop_ln", "push_it",
-                                       "desc_ln", "exact"};
+    if (std::getenv("OCTPT_PROFILE_LANES")) {  // diagnostic builds (-DOCTPT_PROFILE_LANES) fill words 8..18
+        static const char *names[11] = {"iters", "active", "leaf_it", "leaf_ln", "pop_it", "pop_ln", "push_it",
+                                        "desc_ln", "exact", "fold_it", "fold_ln"};
         std::fprintf(stderr, "octpt lanes:");
-        for (uint32_t i = 0; i < 9; ++i) {
+        for (uint32_t i = 0; i < 11; ++i) {
             unsigned long long x = 0;
             for (uint32_t r = 0; r < kSegs; ++r) x += rows[r * kStatRow + 8 + i];
             std::fprintf(stderr, " %s=%llu", names[i], x);

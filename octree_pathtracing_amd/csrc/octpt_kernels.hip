@@ -223,7 +223,8 @@ struct Esvo {
 struct Counters {
     uint32_t paths, segs, steps, sph, cub, shade, tex;
 #ifdef OCTPT_PROFILE_LANES  // diagnostic builds: per-wave lane occupancy of extend's step (stat words 8..)
-    uint32_t p_iters, p_active, p_leaf_it, p_leaf_ln, p_pop_it, p_pop_ln, p_push_it, p_desc_ln, p_exact;
+    uint32_t p_iters, p_active, p_leaf_it, p_leaf_ln, p_pop_it, p_pop_ln, p_push_it, p_desc_ln, p_exact, p_fold_it,
+        p_fold_ln;
 #endif
 };
 
@@ -606,6 +607,10 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 
+#ifndef OCTPT_FOLD
+#define OCTPT_FOLD 1  // absent-sibling fold in esvo_step (A/B: -DOCTPT_FOLD=0)
+#endif
+
 
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
 // common single-primitive leaf (one dependent load fewer).  t_accept = t_exit_w + CELL_TOL * cell_w.
@@ -743,7 +748,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     if (cx) E.pos.x = E.pos.x + delta;
     if (cy) E.pos.y = E.pos.y + delta;
     if (cz) E.pos.z = E.pos.z + delta;
-    const uint32_t step_mask = (cx ? 1u : 0u) | (cy ? 2u : 0u) | (cz ? 4u : 0u);
+    uint32_t step_mask = (cx ? 1u : 0u) | (cy ? 2u : 0u) | (cz ? 4u : 0u);
     // push: level = scale - (OCTREE_MAX_SCALE - depth) = exponent(scale_exp2) - 127 + depth is in
     // [1, depth) for a descend: leaf cells (level 0) are never descended from, and a pop always rises
     // at least one level above them, so level 0 is never written or read and LDS holds levels
@@ -758,11 +763,41 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     E.t_max = descend ? tv_max : E.t_max;
     E.t_min = descend ? E.t_min : tc_max;
     E.idx = descend ? step_mask : (E.idx ^ step_mask);
+    bool pop = !descend && (E.idx & step_mask) != 0u;
+#if OCTPT_FOLD
+    // Absent-sibling fold: when the child this step moved to is absent, the reference's next
+    // iteration (:127-141, then :249-299) only advances past it.  That iteration is run here, as an
+    // exact replica (same t_corner / tc_max / step_mask operations, counted in E.iter, same stop
+    // tests), so the wave does not pay a whole loop iteration for it.  44 % of C3's iterations are
+    // such advances; folding the first of each run leaves 72 % of the iterations (tools/esvo_trace.py).
+    // A fold that leaves the parent pops below, exactly as that iteration would.
+#pragma unroll
+    for (int k = 0; k < OCTPT_FOLD; ++k) {  // OCTPT_FOLD folds at most per step
+    const bool fold = !leaf_hit & !stopped & !pop & (((E.pmask >> (E.idx ^ E.mirror)) & 1u) == 0u) &
+                      (E.iter < OCTREE_MAX_STEPS) & !(E.t_min > max_dst);
+#ifdef OCTPT_PROFILE_LANES
+    prof_wave(cnt.p_fold_it, cnt.p_fold_ln, fold);
+#endif
+    if (fold) {
+        E.iter += 1u;
+        const v3 tf = vsub(vmul(E.pos, E.t_coef), E.t_bias);
+        const float tf_max = tmin3(tf);
+        const bool fx = tf.x <= tf_max, fy = tf.y <= tf_max, fz = tf.z <= tf_max;
+        if (fx) E.pos.x = E.pos.x - E.scale_exp2;
+        if (fy) E.pos.y = E.pos.y - E.scale_exp2;
+        if (fz) E.pos.z = E.pos.z - E.scale_exp2;
+        step_mask = (fx ? 1u : 0u) | (fy ? 2u : 0u) | (fz ? 4u : 0u);
+        E.t_min = tf_max;
+        E.idx ^= step_mask;
+        pop = (E.idx & step_mask) != 0u;
+    }
+    }
+#endif
     bool escaped = false;
 #ifdef OCTPT_PROFILE_LANES
-    prof_wave(cnt.p_pop_it, cnt.p_pop_ln, !descend && (E.idx & step_mask) != 0u);
+    prof_wave(cnt.p_pop_it, cnt.p_pop_ln, pop);
 #endif
-    if (!descend && (E.idx & step_mask) != 0u) {  // pop (:262-299)
+    if (pop) {  // pop (:262-299)
         // the three axes' differing bits are selected, not branched on (no exec-mask region)
         const uint32_t dx = __float_as_uint(E.pos.x) ^ __float_as_uint(E.pos.x + E.scale_exp2);
         const uint32_t dy = __float_as_uint(E.pos.y) ^ __float_as_uint(E.pos.y + E.scale_exp2);
@@ -1180,10 +1215,10 @@ __device__ inline void flush_counters(const Counters &cnt, unsigned long long *s
     return;
 #endif
 #ifdef OCTPT_PROFILE_LANES
-    constexpr int kN = kStatCount + 1 + 9;
+    constexpr int kN = kStatCount + 1 + 11;
     const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex, 0u,
                                cnt.p_iters, cnt.p_active, cnt.p_leaf_it, cnt.p_leaf_ln, cnt.p_pop_it, cnt.p_pop_ln,
-                               cnt.p_push_it, cnt.p_desc_ln, cnt.p_exact};
+                               cnt.p_push_it, cnt.p_desc_ln, cnt.p_exact, cnt.p_fold_it, cnt.p_fold_ln};
 #else
     constexpr int kN = kStatCount;
     const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};

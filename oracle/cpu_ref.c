@@ -647,6 +647,26 @@ static int leaf_test(ctx_t *c, const ray_t *r, uint32_t leaf, float t_exit_w, fl
     return found;
 }
 
+#ifdef REF_ESVO_TRACE
+/* diagnostic build only (tools/esvo_trace.py): one byte per ESVO iteration, single-threaded renders.
+ * low 3 bits: 0 advance over an absent child, 1 leaf test missed, 2 leaf hit, 3 descend, 4 advance
+ * past a present child not entered; 8 = the advance popped; 16 = first iteration of a ray */
+static uint8_t *g_trace;
+static size_t g_trace_n, g_trace_cap;
+static int g_trace_first;
+static void trace_put(int code) {
+    if (g_trace_n < g_trace_cap) g_trace[g_trace_n++] = (uint8_t)(code | (g_trace_first ? 16 : 0));
+    g_trace_first = 0;
+}
+void ref_esvo_trace_set(uint8_t *buf, size_t cap) { g_trace = buf; g_trace_cap = cap; g_trace_n = 0; }
+size_t ref_esvo_trace_len(void) { return g_trace_n; }
+#define TRACE(c) trace_put(c)
+#define TRACE_BEGIN() (g_trace_first = 1)
+#else
+#define TRACE(c) ((void)0)
+#define TRACE_BEGIN() ((void)0)
+#endif
+
 /* ------------------------------------------------------------------------- */
 /* ESVO traversal: Octree::intersect_octree_path_tracer                        */
 /* src/octree/octree_traversal.rs:54-302                                        */
@@ -690,9 +710,11 @@ static int esvo(ctx_t *c, const ray_t *ray, float max_dst_w, uint32_t *hit_prim,
     for (int i = 0; i < 3; i++)
         if (vget(upper, i) > t_min) { idx ^= 1u << i; vset(&pos, i, 1.5f); }
 
+    TRACE_BEGIN();
     for (int it = 0; it < OCTREE_MAX_STEPS; it++) {                      /* :127 */
         if (max_dst >= 0.0f && t_min > max_dst) break;
         steps++;
+        int tcode = 4;
         v3 t_corner = vsub(vmul(pos, t_coef), t_bias);
         float tc_max = vmin3(t_corner);
         uint32_t cidx = idx ^ mirror;
@@ -703,7 +725,9 @@ static int esvo(ctx_t *c, const ray_t *ray, float max_dst_w, uint32_t *hit_prim,
         if (present && t_min <= t_max) {                                  /* :142 */
             if (is_leaf && t_min >= 0.0f) {                                /* :143 */
                 float cell_w = scale_exp2 / octree_scale;
+                tcode = 1;
                 if (leaf_test(c, ray, payload, tc_max / octree_scale, cell_w, hit_prim, hit)) {
+                    TRACE(2);
                     *steps_out = steps;
                     return 1;
                 }
@@ -721,15 +745,19 @@ static int esvo(ctx_t *c, const ray_t *ray, float max_dst_w, uint32_t *hit_prim,
                     for (int i = 0; i < 3; i++)
                         if (vget(t_center, i) > t_min) { idx ^= 1u << i; vset(&pos, i, vget(pos, i) + scale_exp2); }
                     t_max = tv_max;
+                    TRACE(3);
                     continue;
                 }
             }
         }
+        if (!present) tcode = 0;
         uint32_t step_mask = 0;                                           /* :249-260 advance */
         for (int i = 0; i < 3; i++)
             if (vget(t_corner, i) <= tc_max) { step_mask ^= 1u << i; vset(&pos, i, vget(pos, i) - scale_exp2); }
         t_min = tc_max;
         idx ^= step_mask;
+        TRACE(tcode | ((idx & step_mask) != 0 ? 8 : 0));
+        (void)tcode;
         if ((idx & step_mask) != 0) {                                     /* :262-299 pop */
             uint32_t diff = 0;
             if (step_mask & 1) diff |= f2u(pos.x) ^ f2u(pos.x + scale_exp2);
