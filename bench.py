@@ -40,11 +40,16 @@ METRIC = "Mrays/sec at 1920×1080×256spp; achieved HBM GB/s vs roofline at 1/2/
 
 
 def extend_bytes(st: dict) -> float:
-    """DESIGN.md §8, wf_extend_kernel: 8 B per ESVO iteration (one packed child slot), 16 + 4 B per
-    sphere test (centre/radius float4 + leaf prim index), 24 + 4 B per cuboid test (min/max
-    float4 + float2 + index), 40 B per segment (32-B ray record read + 8-B hit record write)."""
-    return (8.0 * st["esvo_steps"] + 20.0 * st["sphere_tests"] + 28.0 * st["cuboid_tests"]
-            + 40.0 * st["segments"])
+    """SURVEY.md §8(d) for wf_extend_kernel: 8 B per ESVO iteration (one node record:
+    child mask + child payload; reference iterations, the folded ones included), 16 + 4 B per sphere
+    test (centre/radius float4 + leaf prim index), 24 + 4 B per cuboid test (min/max + index).  The
+    wavefront's own queue traffic (extend_queue_bytes) is not in §8(d) and is reported beside it."""
+    return 8.0 * st["esvo_steps"] + 20.0 * st["sphere_tests"] + 28.0 * st["cuboid_tests"]
+
+
+def extend_queue_bytes(st: dict) -> float:
+    """The wavefront's queue traffic in extend: 32-B ray record read + 8-B hit record write per segment."""
+    return 40.0 * st["segments"]
 
 
 def shade_bytes(st: dict) -> float:
@@ -272,6 +277,8 @@ def main():
             "launches": st["extend_launches"],
             "kernel_ms_avg": round(ext_s * 1e3, 4),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "bytes_basis": "SURVEY.md §8(d): 8 B x ESVO iterations + 20 B x sphere tests + 28 B x cuboid tests",
+            "queue_bytes_per_launch": int(extend_queue_bytes(st) / n_ext),
             "share_of_gpu_time": round(st["extend_ms"] / max(st["extend_ms"] + st["shade_ms"], 1e-9), 3),
             "shade": {"kernel": "wf_shade_kernel", "launches": st["shade_launches"],
                       "kernel_ms_avg": round(sh_s * 1e3, 4), "algorithmic_bytes_per_launch": int(sh_bytes),

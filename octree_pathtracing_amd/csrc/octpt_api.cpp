@@ -31,6 +31,8 @@ constexpr uint64_t kDefaultChunkPaths = 1ull << 29;  // 4K: 64-spp chunks (C5 46
                                                     // (C3 = 530 M paths = one chunk: one drain tail)
 constexpr uint32_t kLookahead = 3;                  // host steering: iterations queued ahead of the check
 constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (57 GB of queues + path state)
+constexpr uint32_t kMaxPool = 1u << 30;              // the sun-sampling planes index 4 * pool slots in uint32
+constexpr uint32_t kMinPool = 1u << 20;              // floor of the out-of-memory fallback (halving)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
 constexpr uint32_t kDefaultRefill = 0;               // extend: idle lanes before a wave refills (0: adaptive)
 
@@ -472,19 +474,33 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
         ctx->wave_allocs.clear();
         ctx->pool = 0;
         WaveBuffers &B = ctx->wb;
-        B.seg_cap = (uint32_t)seg_cap_for(pool);
-        const size_t qlen = (size_t)kSegs * B.seg_cap;  // queue positions
-        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray0[0]));
-        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray0[1]));
-        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray1[0]));
-        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.ray1[1]));
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pa));
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pb));
-        HIP_TRY(ctx, wave_alloc(ctx, pool, &B.pc));
-        B.pool = (uint32_t)pool;
-        HIP_TRY(ctx, wave_alloc(ctx, qlen, &B.hit));
-        HIP_TRY(ctx, wave_alloc(ctx, kCtrlWords, &B.ctrl));
-        ctx->pool = pool;
+        // queues + path state (112 B per slot).  When the device cannot hold them (another tenant,
+        // the host application's own allocations) the pool is halved down to kMinPool: a smaller
+        // pool renders the same frame in more extend launches
+        size_t want = pool;
+        for (;;) {
+            B.seg_cap = (uint32_t)seg_cap_for(want);
+            const size_t qlen = (size_t)kSegs * B.seg_cap;  // queue positions
+            hipError_t e = wave_alloc(ctx, qlen, &B.ray0[0]);
+            if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.ray0[1]);
+            if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.ray1[0]);
+            if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.ray1[1]);
+            if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pa);
+            if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pb);
+            if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pc);
+            if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.hit);
+            if (e == hipSuccess) e = wave_alloc(ctx, kCtrlWords, &B.ctrl);
+            if (e == hipSuccess) break;
+            for (void *p : ctx->wave_allocs) (void)hipFree(p);
+            ctx->wave_allocs.clear();
+            (void)hipGetLastError();
+            if (e != hipErrorOutOfMemory || want <= kMinPool) return hip_fail(ctx, e, "wave buffers");
+            want = std::max<size_t>(want / 2, kMinPool);
+        }
+        if (want < pool)
+            std::fprintf(stderr, "octpt: %zu path slots did not fit in device memory; using %zu\n", pool, want);
+        B.pool = (uint32_t)want;
+        ctx->pool = want;
     }
     if (color_items > ctx->color_cap) {
         HIP_TRY(ctx, hipDeviceSynchronize());
@@ -552,9 +568,13 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     // a branch-schedule chunk holds whole passes (<= 64 sub-samples each, C20)
     if (R.subs) chunk_spp = std::max(chunk_spp, std::min(64u, R.spp_count));
     const uint64_t chunk_max = (uint64_t)chunk_spp * n_px;
-    const size_t pool = (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max);
-    octpt_status st = ensure_wave(ctx, pool, chunk_max, ctx->S.sun.sun_sampling != 0);
+    if (chunk_max > kMaxChunkPaths)  // a branch pass of 64 sub-samples over > 2^25 pixels
+        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "a branch-schedule pass exceeds the 2^31-item chunk limit");
+    octpt_status st = ensure_wave(ctx, (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max), chunk_max,
+                                  ctx->S.sun.sun_sampling != 0);
     if (st != OCTPT_OK) return st;
+    // the pool actually held (smaller than asked after an out-of-memory fallback)
+    const size_t pool = (size_t)std::min<uint64_t>(std::min<uint64_t>(ctx->pool_cap, chunk_max), ctx->pool);
     int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)];
     if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S);
     const int grid_extend = ctx->num_cu * bpc;
@@ -797,7 +817,7 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return bail(OCTPT_ERR_DEVICE);
     ctx->device = device;
     ctx->num_cu = prop.multiProcessorCount;
-    ctx->pool_cap = env_u32("OCTPT_POOL", kDefaultPool);
+    ctx->pool_cap = std::max<uint32_t>(std::min<uint32_t>(env_u32("OCTPT_POOL", kDefaultPool), kMaxPool), 64u);
     ctx->chunk_cap = std::min<uint64_t>(env_u32("OCTPT_CHUNK", (uint32_t)kDefaultChunkPaths), kMaxChunkPaths);
     // OCTPT_REFILL=n fixes the threshold (clamped to [1, 64]); unset: adaptive per wave (0)
     const char *refill_env = std::getenv("OCTPT_REFILL");
@@ -1301,11 +1321,11 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     unsigned long long v[kStatCount] = {0};
     for (uint32_t r = 0; r < kSegs; ++r)
         for (uint32_t i = 0; i < kStatCount; ++i) v[i] += rows[r * kStatRow + i];
-    if (std::getenv("OCTPT_PROFILE_LANES")) {  // diagnostic builds (-DOCTPT_PROFILE_LANES) fill words 8..18
-        static const char *names[11] = {"iters", "active", "leaf_it", "leaf_ln", "pop_it", "pop_ln", "push_it",
-                                        "desc_ln", "exact", "fold_it", "fold_ln"};
+    if (std::getenv("OCTPT_PROFILE_LANES")) {  // diagnostic builds (-DOCTPT_PROFILE_LANES) fill words 8..20
+        static const char *names[13] = {"iters", "active", "leaf_it", "leaf_ln", "pop_it", "pop_ln", "push_it",
+                                        "desc_ln", "exact", "fold_it", "fold_ln", "dfold_it", "dfold_ln"};
         std::fprintf(stderr, "octpt lanes:");
-        for (uint32_t i = 0; i < 11; ++i) {
+        for (uint32_t i = 0; i < 13; ++i) {
             unsigned long long x = 0;
             for (uint32_t r = 0; r < kSegs; ++r) x += rows[r * kStatRow + 8 + i];
             std::fprintf(stderr, " %s=%llu", names[i], x);

@@ -224,7 +224,7 @@ struct Counters {
     uint32_t paths, segs, steps, sph, cub, shade, tex;
 #ifdef OCTPT_PROFILE_LANES  // diagnostic builds: per-wave lane occupancy of extend's step (stat words 8..)
     uint32_t p_iters, p_active, p_leaf_it, p_leaf_ln, p_pop_it, p_pop_ln, p_push_it, p_desc_ln, p_exact, p_fold_it,
-        p_fold_ln;
+        p_fold_ln, p_dfold_it, p_dfold_ln;
 #endif
 };
 
@@ -610,6 +610,11 @@ enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 #ifndef OCTPT_FOLD
 #define OCTPT_FOLD 1  // absent-sibling fold in esvo_step (A/B: -DOCTPT_FOLD=0)
 #endif
+#ifndef OCTPT_DFOLD
+// descend fold in esvo_step, per instance: measured +4 % extend on C5 (block models, depth 11),
+// +-1 % on C3 / C2 / C4, so only the block-model instance runs it (A/B: -DOCTPT_DFOLD=0 / 1 = all)
+#define OCTPT_DFOLD 3
+#endif
 
 
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
@@ -764,6 +769,42 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     E.t_min = descend ? E.t_min : tc_max;
     E.idx = descend ? step_mask : (E.idx ^ step_mask);
     bool pop = !descend && (E.idx & step_mask) != 0u;
+#if OCTPT_DFOLD
+    // Descend fold: a descend whose chosen child is again an octant the ray enters is followed, in
+    // the reference, by an iteration that only descends (:216-244); 26 % of C3's iterations are such
+    // descend-after-descend pairs (tools/esvo_trace.py).  That iteration is run here as an exact
+    // replica (its own stop tests, t_corner, push and child choice, counted in E.iter); its slot
+    // load depends on this step's, which the other waves of the SIMD hide.
+    if ((OCTPT_DFOLD != 3 || kPrims == kPrimsModels) && descend) {
+        const uint32_t cidx2 = E.idx ^ E.mirror;
+        const v3 tc2 = vsub(vmul(E.pos, E.t_coef), E.t_bias);
+        const float tc2_max = tmin3(tc2);
+        const float tv2_max = tmn(E.t_max, tc2_max);
+        const bool d2 = (((E.pmask >> cidx2) & 0x101u) == 0x001u) & (E.iter < OCTREE_MAX_STEPS) &
+                        !(E.t_min > max_dst) & (E.t_min <= tv2_max);
+#ifdef OCTPT_PROFILE_LANES
+        prof_wave(cnt.p_dfold_it, cnt.p_dfold_ln, d2);
+#endif
+        if (d2) {
+            E.iter += 1u;
+            const uint2 slot2 = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx2) - 1u))];
+            const float half2 = E.scale_exp2 * 0.5f;
+            const v3 X2 = vadd(vscale(E.t_coef, half2), tc2);
+            const bool dx = X2.x > E.t_min, dy = X2.y > E.t_min, dz = X2.z > E.t_min;
+            if (dx) E.pos.x = E.pos.x + half2;
+            if (dy) E.pos.y = E.pos.y + half2;
+            if (dz) E.pos.z = E.pos.z + half2;
+            const uint32_t slot_u2 = (__float_as_uint(E.scale_exp2) >> 23) - 128u + S.depth;
+            if (tc2_max < E.h) stk_write(stk, slot_u2, E.parent, E.t_max, E.pmask);
+            E.h = tc2_max;
+            E.parent = slot2.x;
+            E.pmask = slot2.y;
+            E.scale_exp2 = half2;
+            E.t_max = tv2_max;
+            E.idx = (dx ? 1u : 0u) | (dy ? 2u : 0u) | (dz ? 4u : 0u);
+        }
+    }
+#endif
 #if OCTPT_FOLD
     // Absent-sibling fold: when the child this step moved to is absent, the reference's next
     // iteration (:127-141, then :249-299) only advances past it.  That iteration is run here, as an
@@ -1215,10 +1256,11 @@ __device__ inline void flush_counters(const Counters &cnt, unsigned long long *s
     return;
 #endif
 #ifdef OCTPT_PROFILE_LANES
-    constexpr int kN = kStatCount + 1 + 11;
+    constexpr int kN = kStatCount + 1 + 13;
     const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex, 0u,
                                cnt.p_iters, cnt.p_active, cnt.p_leaf_it, cnt.p_leaf_ln, cnt.p_pop_it, cnt.p_pop_ln,
-                               cnt.p_push_it, cnt.p_desc_ln, cnt.p_exact, cnt.p_fold_it, cnt.p_fold_ln};
+                               cnt.p_push_it, cnt.p_desc_ln, cnt.p_exact, cnt.p_fold_it, cnt.p_fold_ln,
+                               cnt.p_dfold_it, cnt.p_dfold_ln};
 #else
     constexpr int kN = kStatCount;
     const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};

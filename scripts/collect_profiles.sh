@@ -10,5 +10,5 @@ cp $S/trace/run_kernel_stats.csv $DEST/${PREFIX}_kernel_stats.csv
 cp $S/pmc_fetch/run_counter_collection.csv $DEST/${PREFIX}_pmc_fetch.csv
 cp $S/pmc_write/run_counter_collection.csv $DEST/${PREFIX}_pmc_write.csv
 python3 scripts/pmc_summary.py $S/trace $S/pmc_tcc $S/pmc_sq $S/pmc_fetch $S/pmc_write > $DEST/${PREFIX}_summary.txt
-cp $S/pmc_C3.json profiles/pmc_C3.json
+[ -f $S/pmc_C3.json ] && cp $S/pmc_C3.json profiles/pmc_C3.json
 echo "collected $S -> $DEST"

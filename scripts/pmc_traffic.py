@@ -4,7 +4,9 @@ WRITE_SIZE passes (separate passes: the two do not fit one TCC pass).
 Corrections per MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in KiB and count
 L2 memory-side requests (Infinity-Cache hits included, so this upper-bounds HBM bytes); on gfx950
 FETCH_SIZE reports 1/2 of the bytes of wide reads, so it is doubled.
-Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON"""
+The FETCH_SIZE factor defaults to that halving (2); FACTOR overrides it with a calibrated value
+(tools/fetch_calib.hip, profiles/fetch_calib.json) and NOTE says where it came from.
+Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON [FACTOR NOTE]"""
 import collections
 import csv
 import glob
@@ -31,14 +33,19 @@ def per_kernel(d, counter):
 
 def main():
     fetch_dir, write_dir, config, out = sys.argv[1:5]
+    factor = float(sys.argv[5]) if len(sys.argv) > 5 else 2.0
+    note = sys.argv[6] if len(sys.argv) > 6 else "gfx950 FETCH_SIZE halving of 16-B streaming reads"
     ft, fn = per_kernel(fetch_dir, "FETCH_SIZE")
     wt, wn = per_kernel(write_dir, "WRITE_SIZE")
     res = {"config": config, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, python3 bench.py --steps 1",
-           "correction": "bytes = 2 * FETCH_SIZE[KiB] * 1024 + WRITE_SIZE[KiB] * 1024 (gfx950 FETCH_SIZE halving)"}
+           "fetch_factor": factor,
+           "correction": f"bytes = {factor} * FETCH_SIZE[KiB] * 1024 + WRITE_SIZE[KiB] * 1024 ({note})",
+           "raw": {}}
     for k in KERNELS:
         if fn[k] == 0 or wn[k] == 0:
             continue
-        fetch = 2.0 * ft[k] * 1024.0 / fn[k]
+        fetch = factor * ft[k] * 1024.0 / fn[k]
+        res["raw"][k] = {"fetch_size_kib_per_launch": ft[k] / fn[k], "write_size_kib_per_launch": wt[k] / wn[k]}
         write = wt[k] * 1024.0 / wn[k]
         res[k] = {"launches": fn[k], "fetch_bytes_per_launch": int(fetch), "write_bytes_per_launch": int(write),
                   "bytes_per_launch": int(fetch + write)}

@@ -302,6 +302,27 @@ def test_c3_fullsize_band(torch_cuda, renderer):
     assert rel_err(acc[r0:r1], racc[r0:r1]).max() <= REL_TOL_FORWARD
 
 
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_4k_fullsize_band(torch_cuda, renderer, name):
+    """The two 4K configs at full 3840x2160, 1 spp: the whole frame is finite and non-negative and
+    a 16-row band through the middle of the frame matches the oracle exactly in per-pixel segment
+    counts and within the forward tolerance in radiance (as test_c3_fullsize_band)."""
+    from octree_pathtracing_amd import scene as S
+    from oracle import cpu_ref
+
+    sc, cam, rs = S.make_config(name)
+    assert (rs.width, rs.height) == (3840, 2160)
+    rs.spp = 1
+    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    assert np.all(np.isfinite(acc)) and acc[..., :3].min() >= 0
+    assert st["paths"] == rs.width * rs.height
+    r0, r1 = rs.height // 2 - 8, rs.height // 2 + 8
+    racc, rsegs, _ = cpu_ref.render(sc, cam, rs.width, rs.height, 1, max_depth=rs.max_depth, seed=rs.seed,
+                                    forward=True, rows=(r0, r1), threads=16)
+    assert np.array_equal(segs[r0:r1], rsegs[r0:r1])
+    assert rel_err(acc[r0:r1], racc[r0:r1]).max() <= REL_TOL_FORWARD
+
+
 def test_c3_grazing_self_hit_regression(torch_cuda, renderer):
     """C3 pixel (269, 770), sample 22: a grazing ray re-hits its own sphere at a chord that rounds
     to zero and the transparent-skip `continue` (path_tracer.rs:52-54) never ends.  Contract C15
