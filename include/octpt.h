@@ -216,6 +216,14 @@ const char *octpt_last_error(const octpt_ctx *ctx);
 /* --- RenderingBackend surface ----------------------------------------------- */
 /* set_scene (gpu_renderer.rs:662-669 -> create_pipeline :201-557): validates and uploads */
 octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *scene);
+/* set_scene with the octree built on the device and kept there (the reference's
+ * flattener octree_to_gpu_data, gpu_octree.rs:28-76, is todo!()).  The scene's octree fields
+ * (octants, octant_count, root, leaf_*) must be NULL / 0; `depth` is the build depth and flags are
+ * the builder's (OCTPT_BUILD_COMPACT).  The primitives are uploaded once, voxelised by the GPU
+ * builder and its arrays packed into the device node slots in place: the resulting device scene is
+ * the one octpt_scene_upload makes from octpt_build_octree_ex's octree, with no round trip through
+ * host memory. */
+octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *scene, uint32_t flags);
 /* set_camera / get_camera (renderer_trait.rs:20-21) */
 octpt_status octpt_set_camera(octpt_ctx *ctx, const octpt_camera *camera);
 octpt_status octpt_get_camera(const octpt_ctx *ctx, octpt_camera *camera);

@@ -159,6 +159,7 @@ SIGNATURES = {
     "octpt_destroy": (None, [_vp]),
     "octpt_last_error": (C.c_char_p, [_vp]),
     "octpt_scene_upload": (_i32, [_vp, C.POINTER(SceneDesc)]),
+    "octpt_scene_build_device": (_i32, [_vp, C.POINTER(SceneDesc), _u32]),
     "octpt_set_camera": (_i32, [_vp, C.POINTER(Camera)]),
     "octpt_get_camera": (_i32, [_vp, C.POINTER(Camera)]),
     "octpt_render": (_i32, [_vp, C.POINTER(RenderParams), _vp, _vp]),

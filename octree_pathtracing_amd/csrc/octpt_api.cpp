@@ -273,13 +273,21 @@ DevQuad make_dev_quad(const octpt_quad &x) {
     return q;
 }
 
-// masks (out): every octant's child mask in the reader form (C21)
-octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d, std::vector<uint16_t> &masks) {
+octpt_status validate_tables(octpt_ctx *ctx, const octpt_scene_desc *d);
+
+// the checks that precede the octree's: version, depth, non-empty tables, primitive pointers.
+// with_octree = false (octpt_scene_build_device): the octree fields must be NULL / 0
+octpt_status validate_head(octpt_ctx *ctx, const octpt_scene_desc *d, bool with_octree) {
     if (!d) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene is NULL");
     if (d->abi_version != OCTPT_ABI_VERSION) return fail(ctx, OCTPT_ERR_INVALID_ARG, "scene abi_version mismatch");
     if (d->depth < 1 || d->depth > kMaxDepth) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree depth must be in [1, 21]");
-    if (!d->octants || d->octant_count == 0 || d->root >= d->octant_count)
-        return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree has no root octant");
+    if (with_octree) {
+        if (!d->octants || d->octant_count == 0 || d->root >= d->octant_count)
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree has no root octant");
+    } else if (d->octants || d->octant_count || d->root || d->leaf_first || d->leaf_count || d->leaf_table_size ||
+               d->leaf_prims || d->leaf_prim_count) {
+        return fail(ctx, OCTPT_ERR_INVALID_ARG, "the device build makes the octree: its scene fields must be NULL / 0");
+    }
     if (d->material_count == 0 || !d->materials) return fail(ctx, OCTPT_ERR_INVALID_ARG, "material table is empty");
     if (d->texture_count == 0 || !d->textures) return fail(ctx, OCTPT_ERR_INVALID_ARG, "texture table is empty");
     if (d->leaf_table_size && (!d->leaf_first || !d->leaf_count))
@@ -289,6 +297,13 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d, std::vect
         return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^27 - 1 spheres or cuboids");
     if (d->sphere_count && !d->spheres) return fail(ctx, OCTPT_ERR_INVALID_ARG, "spheres is NULL");
     if (d->cuboid_count && !d->cuboids) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboids is NULL");
+    return OCTPT_OK;
+}
+
+// masks (out): every octant's child mask in the reader form (C21)
+octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d, std::vector<uint16_t> &masks) {
+    octpt_status st = validate_head(ctx, d, true);
+    if (st != OCTPT_OK) return st;
     // both octant encodings are accepted (C21): (present, leaf bit) = (1,0) or set_mask_for's (0,1)
     masks.resize(d->octant_count);
     for (uint32_t n = 0; n < d->octant_count; ++n) {
@@ -322,6 +337,11 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d, std::vect
             return fail(ctx, OCTPT_ERR_INVALID_ARG, "sphere index out of range");
         }
     }
+    return validate_tables(ctx, d);
+}
+
+// primitive materials, block models, materials and textures
+octpt_status validate_tables(octpt_ctx *ctx, const octpt_scene_desc *d) {
     for (uint32_t s = 0; s < d->sphere_count; ++s)
         if (d->spheres[s].material >= d->material_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "sphere material out of range");
     for (uint32_t c = 0; c < d->cuboid_count; ++c)
@@ -361,6 +381,126 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d, std::vect
             return fail(ctx, OCTPT_ERR_INVALID_ARG, "unknown texture kind");
         }
     }
+    return OCTPT_OK;
+}
+
+// The octree-independent part of a scene upload: primitive tables (host_prims; the device build
+// writes them itself), block models (C19), materials, textures, LUTs and the sun.  S's octree
+// fields are set by the caller.
+octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_prims, DevScene &S) {
+    if (host_prims) {
+        std::vector<float4> sph(d->sphere_count);
+        std::vector<uint32_t> sph_mat(d->sphere_count);
+        for (uint32_t s = 0; s < d->sphere_count; ++s) {
+            const octpt_sphere &x = d->spheres[s];
+            sph[s] = make_float4(x.center[0], x.center[1], x.center[2], x.radius);
+            sph_mat[s] = x.material;
+        }
+        std::vector<float4> cmin(d->cuboid_count);
+        std::vector<float2> cmax(d->cuboid_count);
+        std::vector<uint32_t> cmat((size_t)d->cuboid_count * 6);
+        for (uint32_t c = 0; c < d->cuboid_count; ++c) {
+            const octpt_cuboid &x = d->cuboids[c];
+            cmin[c] = make_float4(x.min[0], x.min[1], x.min[2], x.max[0]);
+            cmax[c] = make_float2(x.max[1], x.max[2]);
+            std::memcpy(&cmat[(size_t)c * 6], x.face_material, 24);
+        }
+        float4 *d_sph, *d_cmin;
+        float2 *d_cmax;
+        uint32_t *d_sph_mat, *d_cmat;
+        HIP_TRY(ctx, upload(ctx, sph.data(), sph.size(), &d_sph));
+        HIP_TRY(ctx, upload(ctx, sph_mat.data(), sph_mat.size(), &d_sph_mat));
+        HIP_TRY(ctx, upload(ctx, cmin.data(), cmin.size(), &d_cmin));
+        HIP_TRY(ctx, upload(ctx, cmax.data(), cmax.size(), &d_cmax));
+        HIP_TRY(ctx, upload(ctx, cmat.data(), cmat.size(), &d_cmat));
+        S.spheres = d_sph;
+        S.sphere_mat = d_sph_mat;
+        S.cub_a = d_cmin;
+        S.cub_b = d_cmax;
+        S.cub_mat = d_cmat;
+    }
+    // block models (C19): Quad::new (quad.rs:90-114) in glam's f32 operation order
+    bool has_models = false;
+    if (d->cuboid_model)
+        for (uint32_t c = 0; c < d->cuboid_count && !has_models; ++c) has_models = d->cuboid_model[c] != OCTPT_MODEL_NONE;
+    std::vector<DevQuad> quads;
+    std::vector<uint2> models;
+    if (has_models) {
+        quads.resize(d->quad_count);
+        for (uint32_t q = 0; q < d->quad_count; ++q) quads[q] = make_dev_quad(d->quads[q]);
+        models.resize(d->model_count);
+        for (uint32_t m = 0; m < d->model_count; ++m) models[m] = make_uint2(d->models[m].first_quad, d->models[m].quad_count);
+    }
+    float lf[256];
+    uint8_t lb[256];
+    make_luts(lf, lb);
+    std::vector<DevMaterial> mats(d->material_count);
+    for (uint32_t m = 0; m < d->material_count; ++m) {
+        const octpt_material &x = d->materials[m];
+        const octpt_texture &t = d->textures[x.texture_index];
+        DevMaterial dm{};
+        dm.ior = x.ior;
+        dm.specular = x.specular;
+        dm.emittance = x.emittance;
+        dm.roughness = x.roughness;
+        dm.metalness = x.metalness;
+        dm.texture_index = x.texture_index;
+        dm.flags = x.flags;
+        dm.texture_kind = t.kind;
+        if (t.kind == OCTPT_TEXTURE_COLOR) {  // F32Color::from(&U8Color) (colors/mod.rs:280-288)
+            dm.color[0] = lf[t.rgba[0]];
+            dm.color[1] = lf[t.rgba[1]];
+            dm.color[2] = lf[t.rgba[2]];
+            dm.color[3] = (float)t.rgba[3] / 255.0f;
+        }
+        mats[m] = dm;
+    }
+    std::vector<DevTexture> texs(d->texture_count);
+    std::vector<uint8_t> texels;
+    for (uint32_t t = 0; t < d->texture_count; ++t) {
+        const octpt_texture &x = d->textures[t];
+        DevTexture dt{};
+        dt.kind = x.kind;
+        dt.rgba = (uint32_t)x.rgba[0] | ((uint32_t)x.rgba[1] << 8) | ((uint32_t)x.rgba[2] << 16) | ((uint32_t)x.rgba[3] << 24);
+        if (x.kind == OCTPT_TEXTURE_IMAGE) {
+            dt.width = x.width;
+            dt.height = x.height;
+            dt.offset = texels.size();
+            texels.insert(texels.end(), x.pixels, x.pixels + (size_t)x.width * x.height * 4);
+        }
+        texs[t] = dt;
+    }
+    DevMaterial *d_mats;
+    DevTexture *d_texs;
+    uint8_t *d_texels;
+    HIP_TRY(ctx, upload(ctx, mats.data(), mats.size(), &d_mats));
+    HIP_TRY(ctx, upload(ctx, texs.data(), texs.size(), &d_texs));
+    HIP_TRY(ctx, upload(ctx, texels.data(), texels.size(), &d_texels));
+    uint32_t *d_cmodel = nullptr;
+    uint2 *d_models = nullptr;
+    DevQuad *d_quads = nullptr;
+    if (has_models) {
+        HIP_TRY(ctx, upload(ctx, d->cuboid_model, d->cuboid_count, &d_cmodel));
+        HIP_TRY(ctx, upload(ctx, models.data(), models.size(), &d_models));
+        HIP_TRY(ctx, upload(ctx, quads.data(), quads.size(), &d_quads));
+    }
+    S.depth = d->depth;
+    S.has_cuboids = d->cuboid_count ? 1u : 0u;
+    S.octree_scale = ldexpf(1.0f, -(int)d->depth);  // Octree::scale (new_octree.rs:40-42)
+    S.inv_octree_scale = ldexpf(1.0f, (int)d->depth);
+    S.cub_model = d_cmodel;
+    S.models = d_models;
+    S.quads = d_quads;
+    S.has_models = has_models ? 1u : 0u;
+    S.mats = d_mats;
+    S.n_mats = d->material_count;
+    S.texs = d_texs;
+    S.n_texs = d->texture_count;
+    S.texels = d_texels;
+    S.lut_float = ctx->d_lut_float;
+    make_sun(d->sun, lf, S.sun);
+    S.sun.f_sub_surface = d->f_sub_surface;
+    S.emitters = d->emitters_enabled ? 1 : 0;
     return OCTPT_OK;
 }
 
@@ -931,129 +1071,21 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
                 }
             }
         }
-        std::vector<float4> sph(d->sphere_count);
-        std::vector<uint32_t> sph_mat(d->sphere_count);
-        for (uint32_t s = 0; s < d->sphere_count; ++s) {
-            const octpt_sphere &x = d->spheres[s];
-            sph[s] = make_float4(x.center[0], x.center[1], x.center[2], x.radius);
-            sph_mat[s] = x.material;
-        }
-        std::vector<float4> cmin(d->cuboid_count);
-        std::vector<float2> cmax(d->cuboid_count);
-        std::vector<uint32_t> cmat((size_t)d->cuboid_count * 6);
-        for (uint32_t c = 0; c < d->cuboid_count; ++c) {
-            const octpt_cuboid &x = d->cuboids[c];
-            cmin[c] = make_float4(x.min[0], x.min[1], x.min[2], x.max[0]);
-            cmax[c] = make_float2(x.max[1], x.max[2]);
-            std::memcpy(&cmat[(size_t)c * 6], x.face_material, 24);
-        }
-        // block models (C19): Quad::new (quad.rs:90-114) in glam's f32 operation order
-        bool has_models = false;
-        if (d->cuboid_model)
-            for (uint32_t c = 0; c < d->cuboid_count && !has_models; ++c) has_models = d->cuboid_model[c] != OCTPT_MODEL_NONE;
-        std::vector<DevQuad> quads;
-        std::vector<uint2> models;
-        if (has_models) {
-            quads.resize(d->quad_count);
-            for (uint32_t q = 0; q < d->quad_count; ++q) quads[q] = make_dev_quad(d->quads[q]);
-            models.resize(d->model_count);
-            for (uint32_t m = 0; m < d->model_count; ++m) models[m] = make_uint2(d->models[m].first_quad, d->models[m].quad_count);
-        }
-        float lf[256];
-        uint8_t lb[256];
-        make_luts(lf, lb);
-        std::vector<DevMaterial> mats(d->material_count);
-        for (uint32_t m = 0; m < d->material_count; ++m) {
-            const octpt_material &x = d->materials[m];
-            const octpt_texture &t = d->textures[x.texture_index];
-            DevMaterial dm{};
-            dm.ior = x.ior;
-            dm.specular = x.specular;
-            dm.emittance = x.emittance;
-            dm.roughness = x.roughness;
-            dm.metalness = x.metalness;
-            dm.texture_index = x.texture_index;
-            dm.flags = x.flags;
-            dm.texture_kind = t.kind;
-            if (t.kind == OCTPT_TEXTURE_COLOR) {  // F32Color::from(&U8Color) (colors/mod.rs:280-288)
-                dm.color[0] = lf[t.rgba[0]];
-                dm.color[1] = lf[t.rgba[1]];
-                dm.color[2] = lf[t.rgba[2]];
-                dm.color[3] = (float)t.rgba[3] / 255.0f;
-            }
-            mats[m] = dm;
-        }
-        std::vector<DevTexture> texs(d->texture_count);
-        std::vector<uint8_t> texels;
-        for (uint32_t t = 0; t < d->texture_count; ++t) {
-            const octpt_texture &x = d->textures[t];
-            DevTexture dt{};
-            dt.kind = x.kind;
-            dt.rgba = (uint32_t)x.rgba[0] | ((uint32_t)x.rgba[1] << 8) | ((uint32_t)x.rgba[2] << 16) | ((uint32_t)x.rgba[3] << 24);
-            if (x.kind == OCTPT_TEXTURE_IMAGE) {
-                dt.width = x.width;
-                dt.height = x.height;
-                dt.offset = texels.size();
-                texels.insert(texels.end(), x.pixels, x.pixels + (size_t)x.width * x.height * 4);
-            }
-            texs[t] = dt;
-        }
-        uint32_t *d_prims, *d_sph_mat, *d_cmat;
         uint2 *d_child;
-        float4 *d_sph, *d_cmin;
-        float2 *d_cmax;
-        DevMaterial *d_mats;
-        DevTexture *d_texs;
-        uint8_t *d_texels;
         HIP_TRY(ctx, upload(ctx, child.data(), child.size(), &d_child));
         float4 *d_leaf_sph = nullptr;
         if (!leaf_sph.empty()) HIP_TRY(ctx, upload(ctx, leaf_sph.data(), leaf_sph.size(), &d_leaf_sph));
+        uint32_t *d_prims;
         HIP_TRY(ctx, upload(ctx, d->leaf_prims, d->leaf_prim_count, &d_prims));
-        HIP_TRY(ctx, upload(ctx, sph.data(), sph.size(), &d_sph));
-        HIP_TRY(ctx, upload(ctx, sph_mat.data(), sph_mat.size(), &d_sph_mat));
-        HIP_TRY(ctx, upload(ctx, cmin.data(), cmin.size(), &d_cmin));
-        HIP_TRY(ctx, upload(ctx, cmax.data(), cmax.size(), &d_cmax));
-        HIP_TRY(ctx, upload(ctx, cmat.data(), cmat.size(), &d_cmat));
-        HIP_TRY(ctx, upload(ctx, mats.data(), mats.size(), &d_mats));
-        HIP_TRY(ctx, upload(ctx, texs.data(), texs.size(), &d_texs));
-        HIP_TRY(ctx, upload(ctx, texels.data(), texels.size(), &d_texels));
-        uint32_t *d_cmodel = nullptr;
-        uint2 *d_models = nullptr;
-        DevQuad *d_quads = nullptr;
-        if (has_models) {
-            HIP_TRY(ctx, upload(ctx, d->cuboid_model, d->cuboid_count, &d_cmodel));
-            HIP_TRY(ctx, upload(ctx, models.data(), models.size(), &d_models));
-            HIP_TRY(ctx, upload(ctx, quads.data(), quads.size(), &d_quads));
-        }
         S.node_child = d_child;
         S.leaf_sph = d_leaf_sph;
+        S.leaf_prims = d_prims;
         S.root = base[d->root];  // traversal "parent" values are child-array bases
         S.root_mask = masks[d->root];
         S.node0_mask = masks[0];  // base[0] == 0: a zeroed stack entry reads octant 0
-        S.depth = d->depth;
         S.n_octants = d->octant_count;
-        S.has_cuboids = d->cuboid_count ? 1u : 0u;
-        S.octree_scale = ldexpf(1.0f, -(int)d->depth);  // Octree::scale (new_octree.rs:40-42)
-        S.inv_octree_scale = ldexpf(1.0f, (int)d->depth);
-        S.leaf_prims = d_prims;
-        S.spheres = d_sph;
-        S.sphere_mat = d_sph_mat;
-        S.cub_a = d_cmin;
-        S.cub_b = d_cmax;
-        S.cub_mat = d_cmat;
-        S.cub_model = d_cmodel;
-        S.models = d_models;
-        S.quads = d_quads;
-        S.has_models = has_models ? 1u : 0u;
-        S.mats = d_mats;
-        S.n_mats = d->material_count;
-        S.texs = d_texs;
-        S.n_texs = d->texture_count;
-        S.texels = d_texels;
-        S.lut_float = ctx->d_lut_float;
-        make_sun(d->sun, lf, S.sun);
-        S.sun.f_sub_surface = d->f_sub_surface;
-        S.emitters = d->emitters_enabled ? 1 : 0;
+        st = upload_tables(ctx, d, true, S);
+        if (st != OCTPT_OK) return st;
         ctx->S = S;
         ctx->has_scene = true;
         return OCTPT_OK;
@@ -1063,6 +1095,75 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
     } catch (...) {
         free_scene(ctx);
         return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in scene upload");
+    }
+}
+
+octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *d, uint32_t flags) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    join_inflight(ctx);
+    if (flags & ~OCTPT_BUILD_COMPACT) return fail(ctx, OCTPT_ERR_INVALID_ARG, "unknown build flags");
+    try {
+        octpt_status st = validate_head(ctx, d, false);
+        if (st != OCTPT_OK) return st;
+        st = validate_tables(ctx, d);
+        if (st != OCTPT_OK) return st;
+        if (pair_bound(d->spheres, d->sphere_count, d->cuboids, d->cuboid_count, d->depth) > kMaxBuildPairs)
+            return fail(ctx, OCTPT_ERR_OOM, "more than 2^31 (cell, primitive) pairs");
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        free_scene(ctx);
+        // the GPU builder (§4) with its result left in the build scratch
+        BuiltOctree unused;
+        DeviceOctree t;
+        bool too_many = false;
+        float ms = 0.0f;
+        hipError_t e = build_octree_gpu(ctx->stream, ctx->build_scratch, d->spheres, d->sphere_count, d->cuboids,
+                                        d->cuboid_count, d->depth, (flags & OCTPT_BUILD_COMPACT) != 0, kMaxBuildPairs,
+                                        unused, too_many, &ms, &t);
+        if (too_many) return fail(ctx, OCTPT_ERR_OOM, "octree build: out of memory");
+        if (e != hipSuccess) return hip_fail(ctx, e, "octree build");
+        ctx->build_ms = ms;
+        // sparse child slots packed on the device, exactly as octpt_scene_upload packs them (§5)
+        if ((uint64_t)t.n_octants * 8u >= 0xFFFFFFF0ull)  // the u32 slot scan cannot wrap
+            return fail(ctx, OCTPT_ERR_UNSUPPORTED, "octree too large for the device build (>= 2^29 octants)");
+        uint32_t *d_base = nullptr, n_slots = 0;
+        HIP_TRY(ctx, slot_bases_gpu(ctx->stream, ctx->build_scratch, t, &d_base, n_slots));
+        ScenePrimTables out{};
+        HIP_TRY(ctx, upload<uint2>(ctx, nullptr, (size_t)n_slots + 8, &out.node_child));  // zeroed: + 8 tail slots
+        if (!d->cuboid_count) HIP_TRY(ctx, upload<float4>(ctx, nullptr, (size_t)n_slots + 8, &out.leaf_sph));
+        HIP_TRY(ctx, upload<uint32_t>(ctx, nullptr, t.n_leaf_prims, &out.leaf_prims));
+        HIP_TRY(ctx, upload<float4>(ctx, nullptr, d->sphere_count, &out.spheres));
+        HIP_TRY(ctx, upload<uint32_t>(ctx, nullptr, d->sphere_count, &out.sphere_mat));
+        HIP_TRY(ctx, upload<float4>(ctx, nullptr, d->cuboid_count, &out.cub_a));
+        HIP_TRY(ctx, upload<float2>(ctx, nullptr, d->cuboid_count, &out.cub_b));
+        HIP_TRY(ctx, upload<uint32_t>(ctx, nullptr, (size_t)d->cuboid_count * 6, &out.cub_mat));
+        HIP_TRY(ctx, fill_scene_gpu(ctx->stream, t, d_base, out));
+        uint16_t root_mask = 0;  // the root is octant 0 (pre-order), base 0
+        HIP_TRY(ctx, hipMemcpy(&root_mask, &t.octants[0].child_mask, sizeof root_mask, hipMemcpyDeviceToHost));
+        DevScene S{};
+        S.node_child = out.node_child;
+        S.leaf_sph = out.leaf_sph;
+        S.leaf_prims = out.leaf_prims;
+        S.spheres = out.spheres;
+        S.sphere_mat = out.sphere_mat;
+        S.cub_a = out.cub_a;
+        S.cub_b = out.cub_b;
+        S.cub_mat = out.cub_mat;
+        S.root = 0u;
+        S.root_mask = root_mask;
+        S.node0_mask = root_mask;
+        S.n_octants = t.n_octants;
+        st = upload_tables(ctx, d, false, S);
+        if (st != OCTPT_OK) return st;
+        ctx->S = S;
+        ctx->has_scene = true;
+        return OCTPT_OK;
+    } catch (const std::bad_alloc &) {
+        free_scene(ctx);
+        return fail(ctx, OCTPT_ERR_OOM, "host allocation failed");
+    } catch (...) {
+        free_scene(ctx);
+        return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception in device scene build");
     }
 }
 

@@ -284,7 +284,7 @@ inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + kBuildBlock - 1) / k
 // slots of the context's grow-only scratch, taken in a fixed order per build
 struct ScratchCursor {
     BuildScratch &s;
-    int next = 0;
+    int next = 0;  // the build takes at most slots 0..25 in a fixed order, slot_bases_gpu 27..29
     template <class T>
     hipError_t get(T **ptr, size_t n) {
         const int k = next++;
@@ -324,7 +324,8 @@ void BuildScratch::release() {
 
 hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const octpt_sphere *spheres, uint32_t ns,
                             const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, bool compact,
-                            uint64_t max_pairs, BuiltOctree &out, bool &too_many, float *ms) {
+                            uint64_t max_pairs, BuiltOctree &out, bool &too_many, float *ms,
+                            DeviceOctree *dev) {
     too_many = false;
     const int32_t N = 1 << depth;
     const uint32_t np = ns + nc;
@@ -367,12 +368,29 @@ hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const oct
     const uint32_t n = (uint32_t)total;
     out.depth = depth;
     out.root = 0u;
+    if (dev) {
+        *dev = DeviceOctree{};
+        dev->spheres = d_sp;
+        dev->cuboids = d_cb;
+        dev->ns = ns;
+        dev->nc = nc;
+        dev->depth = depth;
+    }
     if (n == 0u) {  // empty world: a childless root, as the host builder emits
+        if (ms) *ms = 0.0f;
+        if (dev) {
+            octpt_octant *d_root;
+            BTRY(pool.get(&d_root, 1));
+            BTRY(hipMemsetAsync(d_root, 0, sizeof(octpt_octant), stream));
+            BTRY(hipStreamSynchronize(stream));
+            dev->octants = d_root;
+            dev->n_octants = 1u;
+            return hipSuccess;
+        }
         out.octants.assign(1, octpt_octant{0, 0, {0, 0, 0, 0, 0, 0, 0, 0}});
         out.leaf_first.clear();
         out.leaf_count.clear();
         out.leaf_prims.clear();
-        if (ms) *ms = 0.0f;
         return hipSuccess;
     }
     uint64_t *d_code, *d_code_s;
@@ -466,6 +484,18 @@ hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const oct
         BTRY(hipGetLastError());
     }
     BTRY(hipEventRecord(e1, stream));
+    if (dev) {  // device-resident: the arrays stay in the scratch
+        dev->octants = d_oct;
+        dev->leaf_first = d_first;
+        dev->leaf_count = d_count;
+        dev->leaf_prims = d_prim_s;
+        dev->n_octants = n_oct;
+        dev->n_leaves = L;
+        dev->n_leaf_prims = n;
+        BTRY(hipStreamSynchronize(stream));
+        if (ms) BTRY(hipEventElapsedTime(ms, e0, e1));
+        return hipSuccess;
+    }
     out.octants.resize(n_oct);
     out.leaf_first.resize(L);
     out.leaf_count.resize(L);
@@ -478,6 +508,112 @@ hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const oct
     BTRY(hipStreamSynchronize(stream));
     if (ms) BTRY(hipEventElapsedTime(ms, e0, e1));
     return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// device-resident scene packing (octpt_scene_build_device): the slots octpt_scene_upload packs on
+// the host (octpt_api.cpp), from a DeviceOctree, with no round trip through host memory
+// ---------------------------------------------------------------------------
+namespace {
+
+// present children per octant (the exclusive scan's trailing entry n = 0)
+__global__ __launch_bounds__(kBuildBlock) void slot_count_kernel(const octpt_octant *__restrict__ oct, uint32_t n,
+                                                                 uint32_t *__restrict__ cnt) {
+    const uint32_t o = blockIdx.x * kBuildBlock + threadIdx.x;
+    if (o > n) return;
+    cnt[o] = o < n ? (uint32_t)__popc(oct[o].child_mask & 0xFFu) : 0u;
+}
+
+// octant o's present children from base[o] in child order: octant child = (its base, its mask),
+// single-primitive leaf = (prim id, 1), else (first list index, count); sphere-only scenes also get
+// the single-sphere leaf's sphere beside the slot (leaf_sph, zero elsewhere)
+__global__ __launch_bounds__(kBuildBlock) void slot_fill_kernel(const octpt_octant *__restrict__ oct, uint32_t n,
+                                                                const uint32_t *__restrict__ base,
+                                                                const uint32_t *__restrict__ first,
+                                                                const uint32_t *__restrict__ count,
+                                                                const uint32_t *__restrict__ prims,
+                                                                const octpt_sphere *__restrict__ sp,
+                                                                uint2 *__restrict__ child, float4 *__restrict__ leaf_sph) {
+    const uint32_t o = blockIdx.x * kBuildBlock + threadIdx.x;
+    if (o >= n) return;
+    const octpt_octant v = oct[o];
+    const uint32_t m = v.child_mask;
+    uint32_t k = base[o];
+    for (int i = 0; i < 8; ++i) {
+        if (!((m >> i) & 1u)) continue;
+        const uint32_t c = v.children[i];
+        if (!((m >> (i + 8)) & 1u)) {
+            child[k] = make_uint2(base[c], oct[c].child_mask);
+        } else if (count[c] == 1u) {
+            const uint32_t p = prims[first[c]];
+            child[k] = make_uint2(p, 1u);
+            if (leaf_sph) {
+                const octpt_sphere s = sp[p];
+                leaf_sph[k] = make_float4(s.center[0], s.center[1], s.center[2], s.radius);
+            }
+        } else {
+            child[k] = make_uint2(first[c], count[c]);
+        }
+        ++k;
+    }
+}
+
+__global__ __launch_bounds__(kBuildBlock) void prim_tables_kernel(const octpt_sphere *__restrict__ sp, uint32_t ns,
+                                                                  const octpt_cuboid *__restrict__ cb, uint32_t nc,
+                                                                  float4 *__restrict__ sph, uint32_t *__restrict__ sph_mat,
+                                                                  float4 *__restrict__ cub_a, float2 *__restrict__ cub_b,
+                                                                  uint32_t *__restrict__ cub_mat) {
+    const uint32_t i = blockIdx.x * kBuildBlock + threadIdx.x;
+    if (i < ns) {
+        const octpt_sphere s = sp[i];
+        sph[i] = make_float4(s.center[0], s.center[1], s.center[2], s.radius);
+        sph_mat[i] = s.material;
+    } else if (i < ns + nc) {
+        const uint32_t c = i - ns;
+        const octpt_cuboid b = cb[c];
+        cub_a[c] = make_float4(b.min[0], b.min[1], b.min[2], b.max[0]);
+        cub_b[c] = make_float2(b.max[1], b.max[2]);
+        for (int f = 0; f < 6; ++f) cub_mat[6u * c + f] = b.face_material[f];
+    }
+}
+
+}  // namespace
+
+hipError_t slot_bases_gpu(hipStream_t stream, BuildScratch &scratch, const DeviceOctree &t, uint32_t **d_base,
+                          uint32_t &n_slots) {
+    ScratchCursor pool{scratch, 27};  // after the build's own slots (0..25)
+    const uint32_t n = t.n_octants;
+    uint32_t *d_cnt;
+    BTRY(pool.get(&d_cnt, n + 1));
+    BTRY(pool.get(d_base, n + 1));
+    hipLaunchKernelGGL(slot_count_kernel, dim3(blocks(n + 1)), dim3(kBuildBlock), 0, stream, t.octants, n, d_cnt);
+    BTRY(hipGetLastError());
+    size_t bytes = 0;
+    BTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, d_cnt, *d_base, n + 1, stream));
+    char *d_tmp;
+    BTRY(pool.get(&d_tmp, bytes));
+    BTRY(hipcub::DeviceScan::ExclusiveSum(d_tmp, bytes, d_cnt, *d_base, n + 1, stream));
+    BTRY(hipMemcpyAsync(&n_slots, *d_base + n, sizeof n_slots, hipMemcpyDeviceToHost, stream));
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t fill_scene_gpu(hipStream_t stream, const DeviceOctree &t, const uint32_t *d_base,
+                          const ScenePrimTables &out) {
+    if (t.n_octants) {
+        hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(t.n_octants)), dim3(kBuildBlock), 0, stream, t.octants,
+                           t.n_octants, d_base, t.leaf_first, t.leaf_count, t.leaf_prims, t.spheres, out.node_child,
+                           out.leaf_sph);
+        BTRY(hipGetLastError());
+    }
+    if (t.n_leaf_prims)
+        BTRY(hipMemcpyAsync(out.leaf_prims, t.leaf_prims, (size_t)t.n_leaf_prims * 4, hipMemcpyDeviceToDevice, stream));
+    if (t.ns + t.nc) {
+        hipLaunchKernelGGL(prim_tables_kernel, dim3(blocks((uint64_t)t.ns + t.nc)), dim3(kBuildBlock), 0, stream,
+                           t.spheres, t.ns, t.cuboids, t.nc, out.spheres, out.sphere_mat, out.cub_a, out.cub_b,
+                           out.cub_mat);
+        BTRY(hipGetLastError());
+    }
+    return hipStreamSynchronize(stream);
 }
 
 }  // namespace octpt

@@ -246,9 +246,40 @@ struct BuildScratch {
     void release();
 };
 
-// the octree builder on the device (octpt_build.hip); too_many: more than max_pairs pairs
+// a built octree left on the device (pointers into the BuildScratch, valid until the next build):
+// the same arrays as BuiltOctree, plus the primitives the builder uploaded
+struct DeviceOctree {
+    const octpt_octant *octants = nullptr;
+    const uint32_t *leaf_first = nullptr, *leaf_count = nullptr, *leaf_prims = nullptr;
+    const octpt_sphere *spheres = nullptr;
+    const octpt_cuboid *cuboids = nullptr;
+    uint32_t n_octants = 0, n_leaves = 0, n_leaf_prims = 0, ns = 0, nc = 0, depth = 0;
+};
+
+// the octree builder on the device (octpt_build.hip); too_many: more than max_pairs pairs.
+// dev == nullptr: the result is downloaded into `out`; else it stays on the device in *dev.
 hipError_t build_octree_gpu(hipStream_t stream, BuildScratch &scratch, const octpt_sphere *spheres, uint32_t ns,
                             const octpt_cuboid *cuboids, uint32_t nc, uint32_t depth, bool compact,
-                            uint64_t max_pairs, BuiltOctree &out, bool &too_many, float *ms);
+                            uint64_t max_pairs, BuiltOctree &out, bool &too_many, float *ms,
+                            DeviceOctree *dev = nullptr);
+
+// Device-resident scene packing (octpt_scene_build_device): the sparse child-slot bases of a
+// DeviceOctree (exclusive scan of the present-child counts; *d_base in the scratch, n_octants + 1
+// entries, the last = slot count), then the slots, the single-sphere leaf table and the primitive
+// tables, written exactly as octpt_scene_upload packs them on the host.
+hipError_t slot_bases_gpu(hipStream_t stream, BuildScratch &scratch, const DeviceOctree &t, uint32_t **d_base,
+                          uint32_t &n_slots);
+struct ScenePrimTables {
+    uint2 *node_child;   // n_slots + 8 (the tail zeroed by the caller)
+    float4 *leaf_sph;    // sphere-only scenes, else nullptr
+    uint32_t *leaf_prims;
+    float4 *spheres;
+    uint32_t *sphere_mat;
+    float4 *cub_a;
+    float2 *cub_b;
+    uint32_t *cub_mat;
+};
+hipError_t fill_scene_gpu(hipStream_t stream, const DeviceOctree &t, const uint32_t *d_base,
+                          const ScenePrimTables &out);
 
 }  // namespace octpt

@@ -166,6 +166,15 @@ class HipRenderer:
         self._scene_keep = keep
         self.reset_render()
 
+    def set_scene_built(self, scene: Scene, depth: int, compact: bool = False) -> None:
+        """set_scene with the octree built on this GPU and kept there (octpt_scene_build_device): the
+        device scene equals set_scene(scene) after scene.build_octree(depth, compact=compact), without
+        the host round trip.  scene.octree is left untouched."""
+        desc, keep = scene.to_desc(octree=False, depth=depth)
+        self._check(self._lib.octpt_scene_build_device(self._ctx, C.byref(desc), _lib.BUILD_COMPACT if compact else 0))
+        self._scene_keep = keep
+        self.reset_render()
+
     def render_frame(self, spp_count: int | None = None) -> FrameInFlight:
         """RenderingBackend::render_frame: enqueue the next pass batch, return a FrameInFlight."""
         if self._in_flight is not None:

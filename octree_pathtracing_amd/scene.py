@@ -277,9 +277,10 @@ class Scene:
                         int(st.importance_sampling), int(st.diffuse_sun), int(st.sun_sampling),
                         int(st.strict_direct_light), int(st.sun_luminosity), s.luminosity_pdf)
 
-    def to_desc(self):
-        """octpt_scene_desc for octpt_scene_upload; returns (desc, keepalive)."""
-        if self.octree is None:
+    def to_desc(self, octree: bool = True, depth: int | None = None):
+        """octpt_scene_desc for octpt_scene_upload; returns (desc, keepalive).  octree=False: the
+        octree fields stay NULL / 0 and `depth` is the build depth (octpt_scene_build_device)."""
+        if octree and self.octree is None:
             raise ValueError("scene has no octree: call build_octree(depth) first")
         t = self.octree
         keep = []
@@ -292,10 +293,11 @@ class Scene:
                 return a.ctypes.data_as(C.c_void_p)
             return C.cast(a, C.c_void_p)
 
-        octs = t.octants_struct()
-        lf = np.ascontiguousarray(t.leaf_first, np.uint32)
-        lc = np.ascontiguousarray(t.leaf_count, np.uint32)
-        lp = np.ascontiguousarray(t.leaf_prims, np.uint32)
+        if octree:
+            octs = t.octants_struct()
+            lf = np.ascontiguousarray(t.leaf_first, np.uint32)
+            lc = np.ascontiguousarray(t.leaf_count, np.uint32)
+            lp = np.ascontiguousarray(t.leaf_prims, np.uint32)
         mats = (_lib.Material * len(self.materials))(*[
             _lib.Material(m.ior, m.specular, m.emittance, m.roughness, m.metalness, m.texture_index, m.tint_index, m.flags)
             for m in self.materials])
@@ -310,15 +312,19 @@ class Scene:
                 texs[i].pixels = px.ctypes.data
         desc = _lib.SceneDesc()
         desc.abi_version = _lib.OCTPT_ABI_VERSION
-        desc.octants = ptr(octs)
-        desc.octant_count = t.octant_count
-        desc.root = t.root
-        desc.depth = t.depth
-        desc.leaf_first = ptr(lf)
-        desc.leaf_count = ptr(lc)
-        desc.leaf_table_size = len(lf)
-        desc.leaf_prims = ptr(lp)
-        desc.leaf_prim_count = len(lp)
+        if octree:
+            desc.octants = ptr(octs)
+            desc.octant_count = t.octant_count
+            desc.root = t.root
+            desc.depth = t.depth
+            desc.leaf_first = ptr(lf)
+            desc.leaf_count = ptr(lc)
+            desc.leaf_table_size = len(lf)
+            desc.leaf_prims = ptr(lp)
+            desc.leaf_prim_count = len(lp)
+            keep.append(octs)
+        else:
+            desc.depth = int(depth if depth is not None else (t.depth if t is not None else 0))
         desc.spheres = ptr(self.sphere_structs()) if len(self.spheres) else None
         desc.sphere_count = len(self.spheres)
         desc.cuboids = ptr(self.cuboid_structs()) if len(self.cuboids) else None
@@ -340,7 +346,7 @@ class Scene:
             desc.model_count = len(self.models)
             desc.quads = ptr(qd) if len(qd) else None
             desc.quad_count = len(qd)
-        keep.extend([octs, mats, texs])
+        keep.extend([mats, texs])
         return desc, keep
 
 

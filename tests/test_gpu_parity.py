@@ -39,11 +39,13 @@ def rel_err(a, b):
 
 
 def gpu_render(torch, r, sc, cam, rs, spp_start=0, accum=None, shard=(0, 1), compact=False, megakernel=False,
-               preview=False, branch_count=1):
-    """Device render through octpt_render_device; returns (accum[H,W,4] or compact, seg_count, stats)."""
+               preview=False, branch_count=1, upload=True):
+    """Device render through octpt_render_device; returns (accum[H,W,4] or compact, seg_count, stats).
+    upload=False: render the scene already on the context (octpt_scene_build_device)."""
     from octree_pathtracing_amd.renderer import shard_pixels
 
-    r.set_scene(sc)
+    if upload:
+        r.set_scene(sc)
     r.set_camera(cam)
     r.max_depth, r.seed = rs.max_depth, rs.seed
     r.branch_count = branch_count
