@@ -21,6 +21,10 @@
 #include "octpt_internal.h"
 #include "octpt_mask.h"
 
+#ifndef OCTPT_NODE_CACHE
+#define OCTPT_NODE_CACHE 0  // see octpt_kernels.hip
+#endif
+
 using namespace octpt;
 
 namespace {
@@ -78,6 +82,8 @@ struct octpt_ctx {
     unsigned long long *d_stats = nullptr;
     uint8_t *d_lut_byte = nullptr;
     float *d_lut_float = nullptr;
+    uint4 *d_chain = nullptr;   // start chain of the camera centre ray (DevScene::chain), per render
+    bool start_chain = true;    // OCTPT_START_CHAIN=0 disables the replay (A/B)
     std::vector<EventPair> pending;
     double kernel_ms = 0.0;
     uint64_t launches = 0;
@@ -498,6 +504,7 @@ octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_
     S.n_texs = d->texture_count;
     S.texels = d_texels;
     S.lut_float = ctx->d_lut_float;
+    S.chain = ctx->d_chain;
     make_sun(d->sun, lf, S.sun);
     S.sun.f_sub_surface = d->f_sub_surface;
     S.emitters = d->emitters_enabled ? 1 : 0;
@@ -787,6 +794,10 @@ octpt_status enqueue_render(octpt_ctx *ctx, const DevRender &R, float4 *d_accum,
     ctx->pending.push_back(ev);  // destroyed by get_stats / destroy
     HIP_TRY(ctx, hipEventRecord(ev.start, s));
     octpt_status st = OCTPT_OK;
+    if (OCTPT_START_CHAIN && !megakernel) {  // the start chain of this camera (extend and preview replay it)
+        if (ctx->start_chain) HIP_TRY(ctx, launch_start_chain(ctx->S, ctx->C, ctx->d_chain, s));
+        else HIP_TRY(ctx, hipMemsetAsync(ctx->d_chain, 0, sizeof(uint4), s));
+    }
     if (R.preview) {
         const hipError_t e = launch_preview(ctx->S, ctx->C, R, d_accum, d_seg, ctx->d_stats, s);
         if (e != hipSuccess) st = hip_fail(ctx, e, "preview launch");
@@ -976,6 +987,12 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     if (hipMalloc(&ctx->d_lut_byte, sizeof lb) != hipSuccess) return bail(OCTPT_ERR_OOM);
     if (hipMemcpy(ctx->d_lut_float, lf, sizeof lf, hipMemcpyHostToDevice) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMemcpy(ctx->d_lut_byte, lb, sizeof lb, hipMemcpyHostToDevice) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    if (hipMalloc(&ctx->d_chain, kChainEntries * sizeof(uint4)) != hipSuccess) return bail(OCTPT_ERR_OOM);
+    if (hipMemset(ctx->d_chain, 0, kChainEntries * sizeof(uint4)) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
+    {
+        const char *sc = std::getenv("OCTPT_START_CHAIN");
+        ctx->start_chain = !(sc && sc[0] == '0');
+    }
     *out = ctx;
     return OCTPT_OK;
 }
@@ -1007,6 +1024,7 @@ void octpt_destroy(octpt_ctx *ctx) {
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_lut_float) (void)hipFree(ctx->d_lut_float);
     if (ctx->d_lut_byte) (void)hipFree(ctx->d_lut_byte);
+    if (ctx->d_chain) (void)hipFree(ctx->d_chain);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1029,10 +1047,43 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         // One 8-byte load per descend / leaf visit yields the child's own base and mask.
         std::vector<uint32_t> base(d->octant_count);
         size_t n_slots = 0;
+#if OCTPT_NODE_CACHE
+        // node-cache experiment: the slots of the top OCTPT_NODE_CACHE_LEVELS levels'
+        // octants come first (breadth first), so that extend mirrors [0, n_cached) in LDS
+        std::vector<uint32_t> first;
+        {
+            const uint32_t levels = env_u32("OCTPT_NODE_CACHE_LEVELS", 2u);
+            std::vector<uint32_t> frontier{d->root};
+            std::vector<char> taken(d->octant_count, 0);
+            for (uint32_t l = 0; l < levels && !frontier.empty(); ++l) {
+                size_t add = 0;
+                for (uint32_t o : frontier) add += (size_t)__builtin_popcount(masks[o] & 0xFFu);
+                if (n_slots + add > 1024u) break;  // LDS budget of the cache (8 KB)
+                std::vector<uint32_t> next;
+                for (uint32_t o : frontier) {
+                    if (taken[o]) continue;
+                    taken[o] = 1;
+                    first.push_back(o);
+                    base[o] = (uint32_t)n_slots;
+                    n_slots += (size_t)__builtin_popcount(masks[o] & 0xFFu);
+                    for (int i = 0; i < 8; ++i)
+                        if (((masks[o] >> i) & 1) && !((masks[o] >> (i + 8)) & 1)) next.push_back(d->octants[o].children[i]);
+                }
+                frontier.swap(next);
+            }
+            S.n_cached = (uint32_t)n_slots;
+            for (uint32_t n = 0; n < d->octant_count; ++n) {
+                if (taken[n]) continue;
+                base[n] = (uint32_t)n_slots;
+                n_slots += (size_t)__builtin_popcount(masks[n] & 0xFFu);
+            }
+        }
+#else
         for (uint32_t n = 0; n < d->octant_count; ++n) {
             base[n] = (uint32_t)n_slots;
             n_slots += (size_t)__builtin_popcount(masks[n] & 0xFFu);
         }
+#endif
         if (n_slots >= 0xFFFFFFFFull) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree too large");
         // + 8 zero slots: a child index computed for an absent child of the last octant stays in bounds
         std::vector<uint2> child(n_slots + 8, make_uint2(0u, 0u));

@@ -83,6 +83,7 @@ struct DevScene {
     const float4 *leaf_sph;         // parallel to node_child: the sphere of a single-sphere leaf slot
     uint32_t root, root_mask, node0_mask, depth, n_octants;  // root = the root octant's base
     uint32_t has_cuboids;
+    uint32_t n_cached;              // slots [0, n_cached) mirrored in LDS (OCTPT_NODE_CACHE experiment), else 0
     float octree_scale;             // 2^-depth
     float inv_octree_scale;         // 2^depth (x / 2^-depth == x * 2^depth exactly)
     const uint32_t *leaf_prims;
@@ -101,6 +102,9 @@ struct DevScene {
     uint32_t n_texs;
     const uint8_t *texels;
     const float *lut_float;         // LUT_TABLE_FLOAT (texture.rs:51-54)
+    // start chain (get_traversal_data's beam start): chain[0].x = n, chain[1 + l] =
+    // (child index, its base, its mask) of the l-th descend of the camera centre ray from the root
+    const uint4 *chain;
     DevSun sun;
     int32_t emitters;
 };
@@ -205,6 +209,13 @@ hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const ui
 hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards,
                           uint32_t stride, float4 *frame, hipStream_t stream);
 int render_blocks_per_cu(uint32_t depth);
+// the start chain of the camera's centre ray (DevScene::chain), one thread.  The replay is compiled
+// out by default: measured -1 % on C3 / C5 and +-0 on preview; -DOCTPT_START_CHAIN=1
+#ifndef OCTPT_START_CHAIN
+#define OCTPT_START_CHAIN 0
+#endif
+constexpr uint32_t kChainEntries = kMaxDepth + 2;
+hipError_t launch_start_chain(const DevScene &S, const DevCamera &C, uint4 *chain, hipStream_t stream);
 size_t render_lds_bytes(uint32_t depth);
 
 // std::vector allocator that leaves resized elements uninitialised: the builders overwrite every

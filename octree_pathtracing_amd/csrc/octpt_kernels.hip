@@ -17,6 +17,10 @@
 // implements as `forward_accumulation`.
 #include "octpt_internal.h"
 
+#ifndef OCTPT_NODE_CACHE
+#define OCTPT_NODE_CACHE 0  // LDS copy of the top octree levels' slots in extend (experiment)
+#endif
+
 namespace octpt {
 namespace {
 
@@ -191,6 +195,9 @@ template <uint32_t kStride>
 struct StackT {
     uint2 *e;
     uint16_t *m;
+#if OCTPT_NODE_CACHE
+    const uint2 *nc;  // LDS copy of node_child[0, S.n_cached): the top octree levels (experiment)
+#endif
 };
 using Stack = StackT<kBlock>;
 
@@ -556,6 +563,9 @@ __device__ __forceinline__ void stk_write(const StackT<kS> &stk, uint32_t slot, 
 template <uint32_t kS = kBlock>
 __device__ __forceinline__ StackT<kS> stack_of(uint2 *lds, uint32_t depth) {
     StackT<kS> s;
+#if OCTPT_NODE_CACHE
+    s.nc = nullptr;  // only wf_extend_kernel loads the cache; the other kernels get n_cached = 0
+#endif
     s.e = lds + threadIdx.x;
     s.m = reinterpret_cast<uint16_t *>(lds + (size_t)(depth - 1u) * kS) + threadIdx.x;
     return s;
@@ -606,6 +616,73 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
+
+// One descend-only ESVO iteration (octree_traversal.rs:216-244, counted in E.iter) into the child
+// whose slot is (its base, its mask); tc / tc_max / tv_max are the current cell's t_corner, its
+// minimum and min(t_max, tc_max).  The same operations as esvo_step's descend.
+template <uint32_t kS>
+__device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uint32_t depth, v3 tc, float tc_max,
+                                             float tv_max, uint2 slot) {
+    E.iter += 1u;
+    const float half = E.scale_exp2 * 0.5f;
+    const v3 X = vadd(vscale(E.t_coef, half), tc);
+    const bool dx = X.x > E.t_min, dy = X.y > E.t_min, dz = X.z > E.t_min;
+    if (dx) E.pos.x = E.pos.x + half;
+    if (dy) E.pos.y = E.pos.y + half;
+    if (dz) E.pos.z = E.pos.z + half;
+    const uint32_t slot_u = (__float_as_uint(E.scale_exp2) >> 23) - 128u + depth;
+    if (tc_max < E.h) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
+    E.h = tc_max;
+    E.parent = slot.x;
+    E.pmask = slot.y;
+    E.scale_exp2 = half;
+    E.t_max = tv_max;
+    E.idx = (dx ? 1u : 0u) | (dy ? 2u : 0u) | (dz ? 4u : 0u);
+}
+
+
+// Start chain (get_traversal_data's beam start, octree_traversal.rs:537-714, meant for
+// CameraUniform.traversal_start_idx, gpu_renderer.rs:579-581).  S.chain holds the descends the
+// camera's centre ray makes from the root.  A ray whose first iterations are descends into the same
+// children runs them here as exact replicas of esvo_step's descend (same stop tests, t-values, push
+// and child choice, counted in E.iter) with the child slots taken from the chain (scalar loads)
+// instead of node_child: coherent primary rays skip the top levels' loads and step overhead.  A lane
+// leaves the replay at the first level where its iteration would not descend into the chain's child.
+template <uint32_t kS>
+__device__ __forceinline__ void esvo_start_chain(const DevScene &S, Esvo &E, const StackT<kS> &stk,
+                                                 const uint4 *__restrict__ chain) {
+#if OCTPT_START_CHAIN
+    const float max_dst = MAX_DST_WORLD * S.octree_scale;
+    const uint32_t n = chain[0].x;  // wave-uniform (LDS)
+    uint4 c = chain[1];
+    for (uint32_t l = 0; l < n; ++l) {
+        const uint4 cn = chain[2u + l];  // the next entry's LDS read overlaps this level (kChainEntries + 1 slots)
+        const v3 tc = vsub(vmul(E.pos, E.t_coef), E.t_bias);
+        const float tc_max = tmin3(tc);
+        const float tv_max = tmn(E.t_max, tc_max);
+        // esvo_step's descend test: the chain's child is an octant of the same parent
+        const bool d = ((E.idx ^ E.mirror) == c.x) & (E.iter < OCTREE_MAX_STEPS) & !(E.t_min > max_dst) &
+                       (E.t_min <= tv_max);
+        if (!d) break;
+        esvo_descend(E, stk, S.depth, tc, tc_max, tv_max, make_uint2(c.y, c.z));
+        c = cn;
+    }
+#endif
+}
+
+// LDS copy of the start chain (kChainEntries + 1 uint4 after the block's stack rows), block-wide
+constexpr uint32_t kChainLdsBytes = OCTPT_START_CHAIN ? (kChainEntries + 1u) * 16u : 0u;
+__device__ __forceinline__ const uint4 *chain_to_lds(const DevScene &S, uint2 *lds) {
+#if OCTPT_START_CHAIN
+    uint4 *c = reinterpret_cast<uint4 *>(lds + (size_t)(S.depth - 1u) * kBlock * 10u / 8u);
+    if (threadIdx.x < kChainEntries) c[threadIdx.x] = S.chain[threadIdx.x];
+    if (threadIdx.x == kChainEntries) c[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    return c;
+#else
+    return nullptr;
+#endif
+}
 
 #ifndef OCTPT_FOLD
 #define OCTPT_FOLD 1  // absent-sibling fold in esvo_step (A/B: -DOCTPT_FOLD=0)
@@ -720,7 +797,11 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const bool descend = (kind == 0x001u) & !stopped & (E.t_min <= tv_max);
     uint2 slot = make_uint2(0u, 0u);
     const uint32_t sidx = E.parent + __popc(E.pmask & ((1u << cidx) - 1u));
+#if OCTPT_NODE_CACHE
+    if (take_leaf || descend) slot = sidx < S.n_cached ? stk.nc[sidx] : S.node_child[sidx];
+#else
     if (take_leaf || descend) slot = S.node_child[sidx];
+#endif
     // sphere-only scenes: a leaf's first sphere is loaded beside its slot (no dependent second load)
     float4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (kPrims == kPrimsSpheres && take_leaf) lsph = S.leaf_sph[sidx];
@@ -786,22 +867,8 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         prof_wave(cnt.p_dfold_it, cnt.p_dfold_ln, d2);
 #endif
         if (d2) {
-            E.iter += 1u;
             const uint2 slot2 = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx2) - 1u))];
-            const float half2 = E.scale_exp2 * 0.5f;
-            const v3 X2 = vadd(vscale(E.t_coef, half2), tc2);
-            const bool dx = X2.x > E.t_min, dy = X2.y > E.t_min, dz = X2.z > E.t_min;
-            if (dx) E.pos.x = E.pos.x + half2;
-            if (dy) E.pos.y = E.pos.y + half2;
-            if (dz) E.pos.z = E.pos.z + half2;
-            const uint32_t slot_u2 = (__float_as_uint(E.scale_exp2) >> 23) - 128u + S.depth;
-            if (tc2_max < E.h) stk_write(stk, slot_u2, E.parent, E.t_max, E.pmask);
-            E.h = tc2_max;
-            E.parent = slot2.x;
-            E.pmask = slot2.y;
-            E.scale_exp2 = half2;
-            E.t_max = tv2_max;
-            E.idx = (dx ? 1u : 0u) | (dy ? 2u : 0u) | (dz ? 4u : 0u);
+            esvo_descend(E, stk, S.depth, tc2, tc2_max, tv2_max, slot2);
         }
     }
 #endif
@@ -1401,6 +1468,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
                                                          unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
     const Stack stk = stack_of(lds_stack, S.depth);
+    const uint4 *chain = chain_to_lds(S, lds_stack);
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     const uint32_t item = blockIdx.x * kBlock + threadIdx.x;
     uint32_t x = 0u, y = 0u;
@@ -1433,6 +1501,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
             const TraceRay tr = trace_ray_of(S, ps);
             Esvo E;
             esvo_begin(S, tr, E, stk);
+            esvo_start_chain(S, E, stk, chain);
             uint32_t prim = kPrimNone;
             PrimHit h;
             int rs;
@@ -1461,6 +1530,35 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
         if (segcount) segcount[ai] += pix_segs;
     }
     flush_counters(cnt, stats);
+}
+
+// The start chain (DevScene::chain) of the camera's centre ray, Camera::get_ray(0, 0) (camera.rs:77-86,
+// the ray gpu_renderer.rs:579-581 hands get_traversal_data): ESVO from the root while its
+// iteration is a descend into an octant child, recording each child index and slot.  One thread.
+__global__ void start_chain_kernel(DevScene S, DevCamera C, uint4 *__restrict__ chain) {
+    if (threadIdx.x != 0u || blockIdx.x != 0u) return;
+    uint2 e_store[kMaxDepth];
+    uint16_t m_store[kMaxDepth];
+    StackT<1> stk{e_store, m_store};  // pushes of the walk go to a private stack
+    const v3 d = vnorm(vscale(V(C.dir[0], C.dir[1], C.dir[2]), C.d_factor));
+    const TraceRay tr = make_trace_ray(S, V(C.eye[0], C.eye[1], C.eye[2]), d, kPrimNone, false);
+    Esvo E;
+    esvo_begin(S, tr, E, stk);
+    const float max_dst = MAX_DST_WORLD * S.octree_scale;
+    uint32_t n = 0u;
+    for (; n + 1u < S.depth; ++n) {  // a chain ends above the leaf cells
+        const v3 tc = vsub(vmul(E.pos, E.t_coef), E.t_bias);
+        const float tc_max = tmin3(tc);
+        const float tv_max = tmn(E.t_max, tc_max);
+        const uint32_t cidx = E.idx ^ E.mirror;
+        const bool d2 = (((E.pmask >> cidx) & 0x101u) == 0x001u) & (E.iter < OCTREE_MAX_STEPS) &
+                        !(E.t_min > max_dst) & (E.t_min <= tv_max);
+        if (!d2) break;
+        const uint2 slot = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx) - 1u))];
+        chain[1u + n] = make_uint4(cidx, slot.x, slot.y, 0u);
+        esvo_descend(E, stk, S.depth, tc, tc_max, tv_max, slot);
+    }
+    chain[0] = make_uint4(n, 0u, 0u, 0u);
 }
 
 // ===========================================================================
@@ -1643,7 +1741,17 @@ template <int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
+#if OCTPT_NODE_CACHE
+    Stack stk = stack_of(lds_stack, S.depth);
+    {  // the top levels' slots (the upload puts them first, DESIGN.md §8 node-cache experiment)
+        uint2 *nc = lds_stack + (size_t)(S.depth - 1u) * kBlock * 10u / 8u + kChainLdsBytes / 8u;
+        for (uint32_t i = threadIdx.x; i < S.n_cached; i += kBlock) nc[i] = S.node_child[i];
+        stk.nc = nc;
+    }
+#else
     const Stack stk = stack_of(lds_stack, S.depth);
+#endif
+    const uint4 *chain = chain_to_lds(S, lds_stack);
     const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
     if (blockIdx.x == 0 && threadIdx.x < kSegs) {  // the other queue is refilled by this iteration's shade
         B.ctrl[ctr_count(q ^ 1u, threadIdx.x)] = 0u;
@@ -1701,6 +1809,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                     tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk);
+                    esvo_start_chain(S, E, stk, chain);
                     active = true;
                     lane_rays++;
                 }
@@ -1955,16 +2064,28 @@ static const void *extend_instance(const DevScene &S) {
     return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsSpheres>);
 }
 
+// stack rows + the start chain (+ the node-cache experiment's slots)
+static size_t extend_lds_bytes(const DevScene &S) {
+    const size_t b = render_lds_bytes(S.depth) + kChainLdsBytes;
+#if OCTPT_NODE_CACHE
+    return b + (size_t)S.n_cached * sizeof(uint2);
+#else
+    return b;
+#endif
+}
+
 int extend_blocks_per_cu(const DevScene &S) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S), kBlock, render_lds_bytes(S.depth)) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S), kBlock, extend_lds_bytes(S)) !=
         hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
 }
 
-hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
+hipError_t launch_preview(const DevScene &S0, const DevCamera &C, const DevRender &R, float4 *accum,
                           uint32_t *segcount, unsigned long long *stats, hipStream_t stream) {
+    DevScene S = S0;
+    S.n_cached = 0;  // only wf_extend_kernel mirrors the top slots in LDS
     const uint32_t grid = (R.total_items + kBlock - 1u) / kBlock;
     // the primitive kinds of the scene pick the instance, as for wf_extend_kernel
     const void *fn = S.has_models ? reinterpret_cast<const void *>(preview_kernel<kPrimsModels>)
@@ -1972,13 +2093,21 @@ hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender
                                      : reinterpret_cast<const void *>(preview_kernel<kPrimsSpheres>);
     void *args[] = {const_cast<DevScene *>(&S), const_cast<DevCamera *>(&C), const_cast<DevRender *>(&R), &accum,
                     &segcount, &stats};
-    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth), stream);
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args,
+                                         render_lds_bytes(S.depth) + kChainLdsBytes, stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
-hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum, uint32_t *segcount,
+hipError_t launch_start_chain(const DevScene &S, const DevCamera &C, uint4 *chain, hipStream_t stream) {
+    hipLaunchKernelGGL(start_chain_kernel, dim3(1), dim3(64), 0, stream, S, C, chain);
+    return hipGetLastError();
+}
+
+hipError_t launch_render(const DevScene &S0, const DevCamera &C, const DevRender &R, float4 *accum, uint32_t *segcount,
                          uint32_t *counter, unsigned long long *stats, int grid, hipStream_t stream) {
+    DevScene S = S0;
+    S.n_cached = 0;  // only wf_extend_kernel mirrors the top slots in LDS
     if (S.sun.sun_sampling)
         hipLaunchKernelGGL(render_kernel<true>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R,
                            accum, segcount, counter, stats);
@@ -1999,7 +2128,7 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
                             unsigned long long *stats, hipStream_t stream) {
     // refill 0: the adaptive threshold
     void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &stats};
-    const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth),
+    const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, extend_lds_bytes(S),
                                          stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
@@ -2021,8 +2150,10 @@ hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t 
     return hipGetLastError();
 }
 
-hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t *last_prim, const float *last_normal,
+hipError_t launch_intersect(const DevScene &S0, const float *rays, const uint32_t *last_prim, const float *last_normal,
                             uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps, hipStream_t stream) {
+    DevScene S = S0;
+    S.n_cached = 0;  // only wf_extend_kernel mirrors the top slots in LDS
     const uint32_t grid = (n + kBlock - 1u) / kBlock;
     hipLaunchKernelGGL(intersect_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, rays,
                        last_prim, last_normal, n, t, prim, normal, steps);

@@ -3,7 +3,7 @@
 The frame's 8x8 pixel tiles are dealt round-robin, tile t -> rank t % N; rank k renders its tiles
 into a compact buffer (OCTPT_RENDER_SHARD_COMPACT: tile-major, 64 pixels per tile, row-major inside
 the tile -- the kernels' item_pixel mapping, octpt_kernels.hip) of `stride` pixels (the largest
-shard), the compact buffers are all-gathered (RCCL over xGMI on the GPUs, gloo in the CPU tests)
+shard), the compact buffers are gathered to rank 0 (RCCL over xGMI on the GPUs, gloo in the CPU tests)
 and rank 0 scatters them back into the frame (octpt_unshard_device on the GPU, unshard_host here).
 Per-pixel RNG streams are keyed by pixel and sample, never by rank, so a sharded render equals the
 unsharded one bit for bit.

@@ -705,7 +705,7 @@ def random_cuboids(seed: int, n: int, world: float, emin: float, emax: float):
     return np.concatenate([lo, np.minimum(lo + ext, F32(world - 0.001))], axis=1).astype(F32)
 
 
-CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny", "blocks")
+CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny", "blocks", "C3-in", "C5-fp")
 
 
 C5_SIDE = 1000  # columns per side: 1,001,225 unit blocks with the exposed-side fill
@@ -753,12 +753,14 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
         sc.sphere_material = _assign_materials(ids, seed, 100)
         cam = Camera.look_at((32.0, 38.0, -28.0), (32.0, 32.0, 32.0))
         rs = RenderSettings(1280, 720, 64, seed=seed)
-    elif name == "C3":
+    elif name in ("C3", "C3-in"):
         ids = primitive_materials(sc)
         depth = 8
         sc.spheres = random_spheres(seed, 10_000, 256.0, 0.5, 2.5)
         sc.sphere_material = _assign_materials(ids, seed, 10_000)
         cam = Camera.look_at((128.0, 150.0, -110.0), (128.0, 128.0, 128.0))
+        if name == "C3-in":  # camera inside the sphere cloud (the start chain's case)
+            cam = Camera.look_at((128.3, 128.7, 127.6), (200.0, 140.0, 60.0))
         rs = RenderSettings(1920, 1080, 256, seed=seed)
     elif name == "C4":
         ids = textured_materials(sc, seed)
@@ -770,7 +772,7 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
         sc.cuboid_material = _assign_materials(ids, seed + 5, 6 * n, stream=21).reshape(n, 6)
         cam = Camera.look_at((512.0, 600.0, -420.0), (512.0, 512.0, 512.0))
         rs = RenderSettings(3840, 2160, 512, seed=seed)
-    elif name == "C5":
+    elif name in ("C5", "C5-fp"):
         depth = 11
         sc.cuboids, sc.cuboid_material = voxel_terrain(sc, seed, C5_SIDE)
         # block models (§8f row 1, C19) on 3 % of the grass / sand surface columns
@@ -780,6 +782,8 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
         place_models(sc, seed, ids_m, tops[keep] + np.array([0, 1, 0]))
         mid = 24 + C5_SIDE / 2
         cam = Camera.look_at((mid, 230.0, 24.0 - 60.0), (mid, 100.0, mid))
+        if name == "C5-fp":  # first-person view inside the world above the terrain (heights < 176)
+            cam = Camera.look_at((300.5, 190.0, 300.5), (800.0, 120.0, 800.0))
         rs = RenderSettings(3840, 2160, 1024, seed=seed)
     else:
         raise ValueError(f"unknown config {name!r}; known: {CONFIGS}")
