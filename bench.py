@@ -60,16 +60,17 @@ def shade_bytes(st: dict) -> float:
 
 
 def load_traffic(config: str):
-    """(bytes per extend launch, source description) from profiles/pmc_<config>.json, or (None, None)."""
+    """(bytes per extend launch, source description, L2 hit rate) from profiles/pmc_<config>.json, or Nones."""
     p = ROOT / "profiles" / f"pmc_{config}.json"
     if p.exists():
         try:
             d = json.loads(p.read_text())
-            b = d.get("wf_extend_kernel", {}).get("bytes_per_launch")
-            return b, f"profiles/pmc_{config}.json: {d.get('correction', '')}"
+            ext = d.get("wf_extend_kernel", {})
+            return ext.get("bytes_per_launch"), f"profiles/pmc_{config}.json: {d.get('correction', '')}", \
+                ext.get("l2_hit_rate")
         except Exception:
-            return None, None
-    return None, None
+            return None, None, None
+    return None, None, None
 
 
 def host_cpu() -> dict:
@@ -242,7 +243,7 @@ def main():
     n_sh = max(st["shade_launches"], 1)
     sh_s = st["shade_ms"] / 1e3 / n_sh
     sh_bytes = shade_bytes(st) / n_sh
-    traffic, traffic_src = load_traffic(args.config)
+    traffic, traffic_src, l2_hit = load_traffic(args.config)
     out = {
         "metric": METRIC,
         "value": round(seg / dt / 1e6, 2),
@@ -251,6 +252,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "msamples_per_s": round(W * H * rs.spp * args.steps / dt / 1e6, 2),  # paths/s
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -273,6 +275,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "l2_hit_rate": l2_hit,
             "kernel": "wf_extend_kernel",
             "launches": st["extend_launches"],
             "kernel_ms_avg": round(ext_s * 1e3, 4),

@@ -6,7 +6,8 @@ L2 memory-side requests (Infinity-Cache hits included, so this upper-bounds HBM 
 FETCH_SIZE reports 1/2 of the bytes of wide reads, so it is doubled.
 The FETCH_SIZE factor defaults to that halving (2); FACTOR overrides it with a calibrated value
 (tools/fetch_calib.hip, profiles/fetch_calib.json) and NOTE says where it came from.
-Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON [FACTOR NOTE]"""
+With TCC_DIR (a --pmc TCC_HIT_sum TCC_MISS_sum pass) the L2 hit rate per kernel is recorded too.
+Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON [FACTOR NOTE [TCC_DIR]]"""
 import collections
 import csv
 import glob
@@ -35,6 +36,7 @@ def main():
     fetch_dir, write_dir, config, out = sys.argv[1:5]
     factor = float(sys.argv[5]) if len(sys.argv) > 5 else 2.0
     note = sys.argv[6] if len(sys.argv) > 6 else "gfx950 FETCH_SIZE halving of 16-B streaming reads"
+    tcc_dir = sys.argv[7] if len(sys.argv) > 7 else None
     ft, fn = per_kernel(fetch_dir, "FETCH_SIZE")
     wt, wn = per_kernel(write_dir, "WRITE_SIZE")
     res = {"config": config, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, python3 bench.py --steps 1",
@@ -49,6 +51,12 @@ def main():
         write = wt[k] * 1024.0 / wn[k]
         res[k] = {"launches": fn[k], "fetch_bytes_per_launch": int(fetch), "write_bytes_per_launch": int(write),
                   "bytes_per_launch": int(fetch + write)}
+    if tcc_dir:
+        ht, _ = per_kernel(tcc_dir, "TCC_HIT_sum")
+        mt, _ = per_kernel(tcc_dir, "TCC_MISS_sum")
+        for k in KERNELS:
+            if k in res and ht[k] + mt[k] > 0:
+                res[k]["l2_hit_rate"] = round(ht[k] / (ht[k] + mt[k]), 4)
     open(out, "w").write(json.dumps(res, indent=1) + "\n")
     print(json.dumps(res, indent=1))
 
