@@ -375,12 +375,17 @@ __device__ __forceinline__ int sphere_decide(float4 sp, const TraceRay &r, bool 
     return kDecideHit;
 }
 
-__device__ __forceinline__ float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6f : 1.0f / d; }
+// Ray::set_direction's clamped 1/d (mod.rs:91-112: |d| < 1e-6 -> 1e6) [C12], taken from ESVO's
+// t_coef = 1 / -|rd| (esvo_begin, [C13]) with no division: where |d| >= 1e-6 (above both clamps,
+// ESVO's 2^-23 and C12's 1e-6) rd = d, and the correctly rounded quotients 1/d and 1/-|d| are equal up
+// to sign, d > 0 being ESVO's mirror bit.  Bit-identical to the three divides (the oracle's form).
+__device__ __forceinline__ v3 inv_dir_of(v3 d, v3 t_coef, uint32_t mirror) {
+    return V(fabsf(d.x) < 1e-6f ? 1.0f / 1e-6f : ((mirror & 1u) ? -t_coef.x : t_coef.x),
+             fabsf(d.y) < 1e-6f ? 1.0f / 1e-6f : ((mirror & 2u) ? -t_coef.y : t_coef.y),
+             fabsf(d.z) < 1e-6f ? 1.0f / 1e-6f : ((mirror & 4u) ? -t_coef.z : t_coef.z));
+}
 
-// Ray::set_direction's clamped 1/d (mod.rs:91-112), derived from the direction [C12]
-__device__ __forceinline__ v3 ray_inv_dir(v3 d) { return V(inv_clamped(d.x), inv_clamped(d.y), inv_clamped(d.z)); }
-
-// AABB::intersects_new (aabb.rs:172-191) [C3]; inv = ray_inv_dir(r.d)
+// AABB::intersects_new (aabb.rs:172-191) [C3]; inv = Ray::inv_dir (inv_dir_of)
 __device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const TraceRay &r, v3 inv, bool self_prim,
                                             PrimHit &h) {
     const v3 tb = vmul(vsub(V(bmin.x, bmin.y, bmin.z), r.o), inv);
@@ -700,8 +705,8 @@ __device__ __forceinline__ const uint4 *chain_to_lds(const DevScene &S, uint2 *l
 // reserve registers, 7 waves/SIMD in wf_extend_kernel; kPrimsBoxes adds cuboids, kPrimsModels
 // block-model cuboids)
 template <int kPrims>
-__device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, uint32_t prim, float t_accept,
-                                          PrimHit &h, Counters &cnt) {
+__device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, const Esvo &E, uint32_t prim,
+                                          float t_accept, PrimHit &h, Counters &cnt) {
     const bool self_prim = prim == r.last_prim;
     bool ok;
     if (kPrims == kPrimsSpheres || !(prim & kPrimCuboidBit)) {
@@ -721,8 +726,8 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
             }
         }
         const float2 cb = S.cub_b[ci];
-        // the slab test's three correctly-rounded divides run for cuboid tests only
-        const v3 inv = ray_inv_dir(r.d);
+        // 1/d without the three correctly-rounded divides: ESVO's t_coef holds the same quotients
+        const v3 inv = inv_dir_of(r.d, E.t_coef, E.mirror);
         ok = cuboid_test(make_float4(ca.x, ca.y, ca.z, 0.0f), make_float4(ca.w, cb.x, cb.y, 0.0f), r, inv, self_prim, h);
     }
     return ok && h.t <= t_accept;
@@ -735,7 +740,7 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
 // kFast (wavefront extend): a single-sphere leaf is decided by sphere_decide, falling back to the
 // exact test only when the estimate lies too close to a threshold; its hit carries the root, not t.
 template <int kPrims = kPrimsModels, bool kFast = false>
-__device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr, float t_accept,
+__device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, const Esvo &E, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt, const float4 *pre = nullptr) {
     uint32_t prim = lr.x;
     if (lr.y != 1u) prim = S.leaf_prims[lr.x];
@@ -758,13 +763,13 @@ __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, uint2 lr,
         cnt.sph++;
         found = sphere_test(*pre, r, prim == r.last_prim, best) && best.t <= t_accept;
     } else {
-        found = prim_test<kPrims>(S, r, prim, t_accept, best, cnt);
+        found = prim_test<kPrims>(S, r, E, prim, t_accept, best, cnt);
     }
     if (found) best_prim = prim;
     for (uint32_t k = 1; k < lr.y; ++k) {
         const uint32_t p = S.leaf_prims[lr.x + k];
         PrimHit hk;
-        if (prim_test<kPrims>(S, r, p, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
+        if (prim_test<kPrims>(S, r, E, p, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
             best = hk;
             best_prim = p;
             found = true;
@@ -816,7 +821,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const float t_accept = tc_max * S.inv_octree_scale + CELL_TOL * cell_w;
         // a hit lane runs the advance below too (its state is discarded): the descend / advance
         // block then needs no exec-mask region of its own
-        leaf_hit = leaf_test<kPrims, kFast>(S, ray, slot, t_accept, prim, h, cnt,
+        leaf_hit = leaf_test<kPrims, kFast>(S, ray, E, slot, t_accept, prim, h, cnt,
                                             kPrims == kPrimsSpheres ? &lsph : nullptr);
     }
     // Descend (:216-244) and advance (:249-260) as one select-based update: every lane computes

@@ -1,6 +1,6 @@
 # scratch GPU command of the current step (run via gpurun from the repo root)
 set -o pipefail
-O=gpurun_out/r02k; mkdir -p $O
+O=gpurun_out/r02l; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
 tail -2 $O/gputest.log
 run() {  # tag config spp [env...]
@@ -9,9 +9,9 @@ run() {  # tag config spp [env...]
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['roofline']['kernel_ms_avg'])" $O/b.json "$tag $cfg" | tee -a $O/ab.txt
 }
 for rep in 1 2; do
-  for cfg in C3:256 C2:64 C4:64 C5:64; do
+  for cfg in C4:64 C5:64 C3:256; do
     c=${cfg%%:*}; s=${cfg##*:}
-    run select $c $s || exit 1
-    run branchy $c $s OCTPT_LIB=build_variants/branchy/liboctpt.so || exit 1
+    run tcoef-inv $c $s || exit 1
+    run divides $c $s OCTPT_LIB=build_variants/base/liboctpt.so || exit 1
   done
 done
