@@ -137,6 +137,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=None, help="override passes per step (default: the config's)")
+    ap.add_argument("--compact", action="store_true",
+                    help="build the octree with OCTPT_BUILD_COMPACT (is_compactable merge, DESIGN.md C22)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: the host's CPU share (host_cpu)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -178,6 +180,8 @@ def main():
     from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
 
     sc, cam, rs = S.make_config(args.config)
+    if args.compact:
+        sc.build_octree(sc.octree.depth, compact=True)
     if args.spp:
         rs.spp = args.spp
     W, H = rs.width, rs.height
@@ -260,7 +264,8 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"{args.config}: {len(sc.spheres)} spheres + {len(sc.cuboids)} cuboids, octree depth "
-                        f"{sc.octree.depth}, {W}x{H}, {rs.spp} spp, max_depth {rs.max_depth}, seed {rs.seed}",
+                        f"{sc.octree.depth}{' (compacted)' if args.compact else ''}, {W}x{H}, {rs.spp} spp, "
+                        f"max_depth {rs.max_depth}, seed {rs.seed}",
             "resolution": [W, H],
             "spp": rs.spp,
             "parallelism": (f"tiles{world}" + ("-gloo" if host_staged else "")) if world > 1 else "single",

@@ -88,6 +88,7 @@ def test_create_without_device(lib):
 
 def test_null_context_calls_fail_cleanly(lib):
     assert lib.octpt_scene_upload(None, None) == _lib.ERR_INVALID_ARG
+    assert lib.octpt_scene_build_device(None, None, 0) == _lib.ERR_INVALID_ARG
     assert lib.octpt_set_camera(None, None) == _lib.ERR_INVALID_ARG
     assert lib.octpt_render(None, None, None, None) == _lib.ERR_INVALID_ARG
     assert lib.octpt_get_stats(None, None) == _lib.ERR_INVALID_ARG
@@ -111,3 +112,20 @@ def test_shard_pixels_partition(lib):
         tiles = ((W + 7) // 8) * ((H + 7) // 8)
         assert sum(counts) == sum(64 * len(range(k, tiles, N)) for k in range(N))
         assert max(counts) - min(counts) <= 64
+
+
+def test_device_build_descriptor():
+    """octpt_scene_build_device's descriptor (Scene.to_desc(octree=False)): octree fields NULL / 0,
+    the build depth set, primitives and tables as for octpt_scene_upload."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, _, _ = S.make_config("tiny", build=False)
+    d, keep = sc.to_desc(octree=False, depth=7)
+    assert not d.octants and d.octant_count == 0 and d.root == 0 and d.depth == 7
+    assert not d.leaf_first and not d.leaf_count and d.leaf_table_size == 0
+    assert not d.leaf_prims and d.leaf_prim_count == 0
+    assert d.sphere_count == len(sc.spheres) and d.cuboid_count == len(sc.cuboids)
+    assert d.material_count == len(sc.materials) and d.texture_count == len(sc.textures)
+    sc.build_octree(5)
+    d2, keep2 = sc.to_desc()
+    assert d2.octants and d2.octant_count == sc.octree.octant_count and d2.depth == 5
