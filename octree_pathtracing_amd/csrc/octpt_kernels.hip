@@ -690,7 +690,12 @@ __device__ __forceinline__ const uint4 *chain_to_lds(const DevScene &S, uint2 *l
 }
 
 #ifndef OCTPT_FOLD
-#define OCTPT_FOLD 1  // absent-sibling fold in esvo_step (A/B: -DOCTPT_FOLD=0)
+#define OCTPT_FOLD 1  // absent-sibling folds per step (A/B: -DOCTPT_FOLD=0)
+#endif
+#ifndef OCTPT_FOLD_MODELS
+// the block-model instance folds up to 2 (C5, depth-11 voxel terrain: +1.9 %; 2 folds everywhere:
+// C3 -2.4 %, C4 -2.9 %, C2 +-0)
+#define OCTPT_FOLD_MODELS 2
 #endif
 #ifndef OCTPT_DFOLD
 // descend fold in esvo_step, per instance: measured +4 % extend on C5 (block models, depth 11),
@@ -884,8 +889,9 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // tests), so the wave does not pay a whole loop iteration for it.  44 % of C3's iterations are
     // such advances; folding the first of each run leaves 72 % of the iterations (tools/esvo_trace.py).
     // A fold that leaves the parent pops below, exactly as that iteration would.
+    constexpr int kFolds = kPrims == kPrimsModels ? OCTPT_FOLD_MODELS : OCTPT_FOLD;
 #pragma unroll
-    for (int k = 0; k < OCTPT_FOLD; ++k) {  // OCTPT_FOLD folds at most per step
+    for (int k = 0; k < kFolds; ++k) {  // kFolds folds at most per step
     const bool fold = !leaf_hit & !stopped & !pop & (((E.pmask >> (E.idx ^ E.mirror)) & 1u) == 0u) &
                       (E.iter < OCTREE_MAX_STEPS) & !(E.t_min > max_dst);
 #ifdef OCTPT_PROFILE_LANES

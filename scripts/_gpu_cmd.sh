@@ -1,13 +1,18 @@
 # scratch GPU command of the current step (run via gpurun from the repo root)
 set -o pipefail
-O=gpurun_out/r02n; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -v --timeout 300 --timeout-method thread > $O/fuzz.log 2>&1; rc=$?
-grep -E "PASS|FAIL|Error|assert" $O/fuzz.log | tail -60
-[ $rc = 0 ] || exit $rc
-for cfg in C3:256 C4:64; do
-  c=${cfg%%:*}; s=${cfg##*:}
-  for mode in "" --compact; do
-    timeout -k 10 300 python -u bench.py --config $c --spp $s --steps 3 --warmup 1 --no-cpu-baseline $mode > $O/b.json 2>> $O/bench.err || exit 1
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); st=d['stats_rank0']; print(sys.argv[2], d['value'], d['roofline']['kernel_ms_avg'], round(st['esvo_steps']/st['segments'],2), round((st['sphere_tests']+st['cuboid_tests'])/st['segments'],3), d['ms_per_step'])" $O/b.json "$c $mode" | tee -a $O/compact.txt
+O=gpurun_out/r02p; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
+tail -2 $O/gputest.log
+run() {  # tag config spp [env...]
+  local tag=$1 cfg=$2 spp=$3; shift 3
+  env "$@" timeout -k 10 300 python -u bench.py --config $cfg --spp $spp --steps 3 --warmup 1 --no-cpu-baseline > $O/b.json 2>> $O/bench.err || return 1
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['roofline']['kernel_ms_avg'])" $O/b.json "$tag $cfg" | tee -a $O/ab.txt
+}
+for rep in 1 2; do
+  for cfg in C5:64 C5-fp:64; do
+    c=${cfg%%:*}; s=${cfg##*:}
+    run fold2m $c $s || exit 1
+    run base $c $s OCTPT_LIB=build_variants/base/liboctpt.so || exit 1
+    run fold3m $c $s OCTPT_LIB=build_variants/fold3m/liboctpt.so || exit 1
   done
 done
