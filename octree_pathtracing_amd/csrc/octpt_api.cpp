@@ -39,6 +39,7 @@ constexpr uint32_t kMaxPool = 1u << 30;              // the sun-sampling planes 
 constexpr uint32_t kMinPool = 1u << 20;              // floor of the out-of-memory fallback (halving)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
 constexpr uint32_t kDefaultRefill = 0;               // extend: idle lanes before a wave refills (0: adaptive)
+constexpr uint32_t kDefaultDrainRays = 4096;         // drain the chunk in one launch below this many queued rays
 
 uint32_t env_u32(const char *name, uint32_t dflt) {
     const char *v = std::getenv(name);
@@ -106,6 +107,7 @@ struct octpt_ctx {
     uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
     hipEvent_t count_ev[kLookahead + 1] = {};
     uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
+    uint32_t drain_rays = kDefaultDrainRays;  // queue length at which the drain takes over (OCTPT_DRAIN_RAYS, 0 = off)
     uint64_t chunk_cap = kDefaultChunkPaths;  // (pixel, sample) items per chunk (OCTPT_CHUNK)
     // one asynchronous frame may be in flight; device-touching calls join it first
     octpt_frame *inflight = nullptr;
@@ -603,8 +605,9 @@ hipError_t wave_alloc(octpt_ctx *ctx, size_t n, T **out) {
     return hipSuccess;
 }
 
-// words from ctr_count(q, 0) through ctr_count(q, kSegs - 1)
-constexpr uint32_t kCountSpan = (kSegs - 1u) * kCtrStride + 1u;
+// host snapshot of the iteration's counters: the whole ctrl block (80 KB: queue counts and heads,
+// chunk item claims), read kLookahead iterations later
+constexpr uint32_t kCountSpan = kCtrlWords;
 
 // queue segment capacity: seed wave w fills segment w % kSegs, so ceil(ceil(pool / 64) / kSegs) waves
 size_t seg_cap_for(size_t pool) { return ((pool + 63) / 64 + kSegs - 1) / kSegs * 64; }
@@ -767,16 +770,37 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             // iteration over an empty queue exits at once).  The queue only empties once every
             // chunk item is claimed: finished paths regenerate in the same shade pass.
             const uint32_t slot = it % (kLookahead + 1);
-            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_count + slot * kCountSpan, B.ctrl + ctr_count(q ^ 1u, 0),
-                                        kCountSpan * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_count + slot * kCountSpan, B.ctrl, kCountSpan * sizeof(uint32_t),
+                                        hipMemcpyDeviceToHost, s));
             HIP_TRY(ctx, hipEventRecord(ctx->count_ev[slot], s));
             if (it >= kLookahead) {
                 const uint32_t old = (it - kLookahead) % (kLookahead + 1);
                 HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[old]));
                 const uint32_t *h = ctx->h_count + old * kCountSpan;
+                const uint32_t q_old = ((it - kLookahead) & 1u) ^ 1u;  // the queue that iteration's shade filled
                 uint64_t queued = 0;
-                for (uint32_t k = 0; k < kSegs; ++k) queued += h[k * kCtrStride];
+                for (uint32_t k = 0; k < kSegs; ++k) queued += h[ctr_count(q_old, k)];
                 if (queued == 0u) break;  // iteration it - kLookahead + 1 onwards had nothing to do
+                // Drain: every chunk item claimed and few rays left, so the queue only shrinks from
+                // here (a ray yields at most one ray, and nothing regenerates).  One launch finishes the
+                // paths in the queue this iteration's shade filled instead of the launch-latency-bound
+                // tail of near-empty iterations; timed as an extend launch.
+                if (queued <= ctx->drain_rays) {
+                    bool exhausted = true;
+                    for (uint32_t k = 0; k < kSegs && exhausted; ++k) {
+                        const uint32_t lo = (uint32_t)(((uint64_t)k * chunk_items) / kSegs);
+                        const uint32_t hi = (uint32_t)(((uint64_t)(k + 1u) * chunk_items) / kSegs);
+                        exhausted = h[ctr_item(k)] >= hi - lo;
+                    }
+                    if (exhausted) {
+                        // one path per wave (wf_drain_kernel), four waves per block
+                        const int grid = (int)std::min<uint64_t>((queued + 3) / 4 + 1, (uint64_t)ctx->num_cu * 16u);
+                        if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
+                        HIP_TRY(ctx, launch_wf_drain(ctx->S, Rc, B, q ^ 1u, grid, ctx->d_stats, s));
+                        if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
+                        break;
+                    }
+                }
             }
         }
         HIP_TRY(ctx, launch_wf_resolve(Rc, B, Rc.spp_count, d_accum, d_seg, s));
@@ -975,6 +999,9 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->refill = (refill_env && *refill_env)
                       ? std::max<uint32_t>(std::min<uint32_t>(env_u32("OCTPT_REFILL", 16u), 64u), 1u)
                       : kDefaultRefill;
+    // OCTPT_DRAIN_RAYS=n: the drain's queue threshold; 0 turns the drain off (A/B)
+    const char *drain_env = std::getenv("OCTPT_DRAIN_RAYS");
+    if (drain_env && *drain_env) ctx->drain_rays = (uint32_t)std::strtoul(drain_env, nullptr, 10);
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);

@@ -198,6 +198,9 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
                             unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
                            uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream);
+// the drain of a chunk's last queued rays (every chunk item claimed): one launch, paths finished in-lane
+hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuffers &B, uint32_t q, int grid,
+                           unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,
                              uint32_t *segcount, hipStream_t stream);
 int extend_blocks_per_cu(const DevScene &S);

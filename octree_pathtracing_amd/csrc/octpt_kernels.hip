@@ -1859,6 +1859,47 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
     flush_counters(cnt, stats);
 }
 
+// Shade of one traced segment (a lane of wf_shade_kernel, and of wf_drain_kernel): the path in the ray
+// record's slot is loaded, its hit record (hr, extend's output) committed and its shading step taken.
+// Returns true when the path continues (its state stored to the slot, the next ray in ps), false when
+// it finished (its colour record written).
+template <bool kNee>
+__device__ __forceinline__ bool shade_lane(const DevScene &S, const DevRender &R, const WaveBuffers &B, float4 r0,
+                                           float4 r1, const uint2 *hit_rec, PathState &ps, uint32_t &slot,
+                                           uint32_t &item, Counters &cnt) {
+    slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
+    load_path(B, slot, r0, r1, ps, item);
+    const bool was_shadow = kNee && ps.shadow;
+    if (was_shadow) load_nee(B, slot, ps);
+    const uint2 hr = *hit_rec;
+    const bool hit = hr.x != kPrimNone;
+    if (hit) {
+        PrimHit h;
+        const uint32_t flags = (hr.x >> 27) & 15u;
+        h.t = __uint_as_float(hr.y);
+        h.f = flags;
+        // a sphere hit record carries its root, decided by extend's estimate: t exactly
+        if (!(hr.x & kPrimCuboidBit)) h.t = sphere_root(S.spheres[hr.x & kPrimIndexMask], ps.o, ps.d, flags & 1u);
+        ps.n = V(0.0f, 0.0f, 0.0f);
+        commit_hit(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
+    }
+    bool cont = shade_segment<kNee>(S, R, ps, hit, cnt);
+    if (cont) cont = begin_segment(ps);
+    if (cont) {
+        store_path(B, slot, ps, item);
+        if (kNee && ps.shadow) {  // a shadow segment follows: new sun sample or the next one
+            if (!was_shadow) store_nee(B, slot, ps);
+            store_att(B, slot, ps);
+        }
+        return true;
+    }
+    // segments this item reports (a branch > 0 reports none of the replayed prefix) and whether the
+    // first reflection split (C20)
+    const uint32_t segs = ps.branch == 0u ? ps.path_segs : (ps.depth ? ps.path_segs - ps.seg_base : 0u);
+    B.color[item] = make_float4(ps.L.x, ps.L.y, ps.L.z, __uint_as_float(segs | (ps.depth ? 0x80000000u : 0u)));
+    return false;
+}
+
 // shade: one lane per traced ray (grid-stride, wave-uniform trip count)
 #ifndef OCTPT_SHADE_WAVES
 #define OCTPT_SHADE_WAVES 1
@@ -1907,44 +1948,61 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
         PathState ps;
         if (valid) {
             const float4 r0 = B.ray0[q][i], r1 = B.ray1[q][i];
-            slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
-            load_path(B, slot, r0, r1, ps, item);
-            const bool was_shadow = kNee && ps.shadow;
-            if (was_shadow) load_nee(B, slot, ps);
-            const uint2 hr = B.hit[i];
-            const bool hit = hr.x != kPrimNone;
-            if (hit) {
-                PrimHit h;
-                const uint32_t flags = (hr.x >> 27) & 15u;
-                h.t = __uint_as_float(hr.y);
-                h.f = flags;
-                // a sphere hit record carries its root, decided by extend's estimate: t exactly
-                if (!(hr.x & kPrimCuboidBit)) h.t = sphere_root(S.spheres[hr.x & kPrimIndexMask], ps.o, ps.d, flags & 1u);
-                ps.n = V(0.0f, 0.0f, 0.0f);
-                commit_hit(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
-            }
-            bool cont = shade_segment<kNee>(S, R, ps, hit, cnt);
-            if (cont) cont = begin_segment(ps);
-            if (cont) {
-                store_path(B, slot, ps, item);
-                if (kNee && ps.shadow) {  // a shadow segment follows: new sun sample or the next one
-                    if (!was_shadow) store_nee(B, slot, ps);
-                    store_att(B, slot, ps);
-                }
-                append = true;
-            } else {
-                // segments this item reports (a branch > 0 reports none of the replayed prefix) and
-                // whether the first reflection split (C20)
-                const uint32_t segs = ps.branch == 0u ? ps.path_segs : (ps.depth ? ps.path_segs - ps.seg_base : 0u);
-                B.color[item] = make_float4(ps.L.x, ps.L.y, ps.L.z,
-                                            __uint_as_float(segs | (ps.depth ? 0x80000000u : 0u)));
-                finished = true;
-            }
+            append = shade_lane<kNee>(S, R, B, r0, r1, B.hit + i, ps, slot, item, cnt);
+            finished = !append;
         }
         // regenerate: finished lanes take the next chunk items (path regeneration)
         if (regen(C, R, B, slot, finished, chunk_items, cur, ps, cnt)) append = true;
         const uint32_t t = wave_ticket(B.ctrl + ctr_count(q ^ 1u, seg), append);
         if (append) store_ray(B, q ^ 1u, seg0 + t, slot, ps);
+    }
+    flush_counters(cnt, stats);
+}
+
+// Drain: once every chunk item is claimed and the queue holds few rays, one launch
+// finishes every queued path in its lane -- trace, shade, trace, ... -- instead of one extend /
+// shade pair per remaining segment: the last ~60 iterations of a chunk are the rare long paths, each
+// a near-empty launch pair bounded by host launch latency (5 ms of C3's 288 ms frame, 13 % of an
+// 8-way shard's).  Every segment goes through the wavefront's own formats and code (extend's
+// esvo_step and hit record, shade_lane, the ray record as store_ray writes it), so results and
+// statistics equal the extend / shade iterations it replaces.  No regeneration: items are exhausted.
+template <int kPrims, bool kNee>
+__global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender R, WaveBuffers B, uint32_t q,
+                                                          unsigned long long *__restrict__ stats) {
+    extern __shared__ uint2 lds_stack[];
+    const Stack stk = stack_of(lds_stack, S.depth);
+    Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    // one path per wave (its lane 0): the paths are at different segments and phases, and one lane
+    // each keeps a wave free of divergence; the grid spreads them over every CU
+    const uint32_t wid = (blockIdx.x * kBlock + threadIdx.x) >> 6, nw = (gridDim.x * kBlock) >> 6;
+    const uint32_t jlim = (threadIdx.x & 63u) == 0u ? 0xFFFFFFFFu : 0u;
+    for (uint32_t k = 0; k < kSegs; ++k) {  // queue q, segment after segment, dealt over the waves
+        const uint32_t n = min(B.ctrl[ctr_count(q, k)], jlim);
+        for (uint32_t j = wid; j < n; j += nw) {
+            float4 r0 = B.ray0[q][k * B.seg_cap + j], r1 = B.ray1[q][k * B.seg_cap + j];
+            for (;;) {
+                const TraceRay tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
+                                                   (__float_as_uint(r1.w) >> 31) != 0u);
+                Esvo E;
+                esvo_begin(S, tr, E, stk);
+                uint32_t prim = kPrimNone;
+                PrimHit h;
+                int rs;
+                do {
+                    rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
+                } while (rs == kStepContinue);
+                cnt.steps += E.iter;
+                cnt.segs++;
+                const uint2 hr = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                PathState ps;
+                uint32_t slot, item;
+                if (!shade_lane<kNee>(S, R, B, r0, r1, &hr, ps, slot, item, cnt)) break;
+                // the next segment's ray record, as store_ray writes it
+                r0 = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.last_prim));
+                r1 = make_float4(ps.d.x, ps.d.y, ps.d.z,
+                                 __uint_as_float(slot | (vdot(ps.d, ps.n) < 0.0f ? 0x80000000u : 0u)));
+            }
+        }
     }
     flush_counters(cnt, stats);
 }
@@ -2151,6 +2209,21 @@ hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRende
     auto kern = S.sun.sun_sampling ? (lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
                                    : (lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuffers &B, uint32_t q, int grid,
+                           unsigned long long *stats, hipStream_t stream) {
+    const bool nee = S.sun.sun_sampling != 0;
+    const void *fn = S.has_models ? (nee ? reinterpret_cast<const void *>(wf_drain_kernel<kPrimsModels, true>)
+                                         : reinterpret_cast<const void *>(wf_drain_kernel<kPrimsModels, false>))
+                     : S.has_cuboids ? (nee ? reinterpret_cast<const void *>(wf_drain_kernel<kPrimsBoxes, true>)
+                                            : reinterpret_cast<const void *>(wf_drain_kernel<kPrimsBoxes, false>))
+                                     : (nee ? reinterpret_cast<const void *>(wf_drain_kernel<kPrimsSpheres, true>)
+                                            : reinterpret_cast<const void *>(wf_drain_kernel<kPrimsSpheres, false>));
+    void *args[] = {const_cast<DevScene *>(&S), const_cast<DevRender *>(&R), const_cast<WaveBuffers *>(&B), &q, &stats};
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth), stream);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

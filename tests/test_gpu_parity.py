@@ -325,6 +325,25 @@ def test_4k_fullsize_band(torch_cuda, renderer, name):
     assert rel_err(acc[r0:r1], racc[r0:r1]).max() <= REL_TOL_FORWARD
 
 
+def test_c3_fullframe_repeatable(torch_cuda, renderer):
+    """The whole headline frame is deterministic: the wavefront's atomics decide only the order in
+    which rays are traced, never a value (RNG streams are keyed by pixel and sample), so two renders
+    of C3 at full size are bit-identical, and so is the frame rendered as two progressive halves."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config("C3")
+    rs.spp = 8
+    a = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    b = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32)) and np.array_equal(a[1], b[1])
+    assert a[2]["segments"] == b[2]["segments"] and a[2]["esvo_steps"] == b[2]["esvo_steps"]
+    rs.spp = 4
+    h1 = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    h2 = gpu_render(torch_cuda, renderer, sc, cam, rs, spp_start=4, accum=h1[0])
+    assert np.array_equal(h2[0].view(np.uint32), a[0].view(np.uint32))
+    assert np.array_equal(h1[1] + h2[1], a[1])
+
+
 def test_c3_grazing_self_hit_regression(torch_cuda, renderer):
     """C3 pixel (269, 770), sample 22: a grazing ray re-hits its own sphere at a chord that rounds
     to zero and the transparent-skip `continue` (path_tracer.rs:52-54) never ends.  Contract C15
