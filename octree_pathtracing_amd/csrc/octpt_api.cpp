@@ -784,8 +784,10 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
                 // Drain: every chunk item claimed and few rays left, so the queue only shrinks from
                 // here (a ray yields at most one ray, and nothing regenerates).  One launch finishes the
                 // paths in the queue this iteration's shade filled instead of the launch-latency-bound
-                // tail of near-empty iterations; timed as an extend launch.
-                if (queued <= ctx->drain_rays) {
+                // tail of near-empty iterations.  Not in the extend timer (rocprof reports it as
+                // wf_drain_kernel); its statistics (<= 4096 paths) stay in the totals.
+                // (not for block-model scenes: their tails are transparent-texel chains, C5 -1 %)
+                if (queued <= ctx->drain_rays && !ctx->S.has_models) {
                     bool exhausted = true;
                     for (uint32_t k = 0; k < kSegs && exhausted; ++k) {
                         const uint32_t lo = (uint32_t)(((uint64_t)k * chunk_items) / kSegs);
@@ -795,9 +797,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
                     if (exhausted) {
                         // one path per wave (wf_drain_kernel), four waves per block
                         const int grid = (int)std::min<uint64_t>((queued + 3) / 4 + 1, (uint64_t)ctx->num_cu * 16u);
-                        if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
                         HIP_TRY(ctx, launch_wf_drain(ctx->S, Rc, B, q ^ 1u, grid, ctx->d_stats, s));
-                        if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
                         break;
                     }
                 }

@@ -1,10 +1,11 @@
 # scratch GPU command of the current step (run via gpurun from the repo root)
 set -o pipefail
-O=gpurun_out/r02x; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
-tail -2 $O/gputest.log
-timeout -k 10 300 python -u scripts/shard_emulation.py --config C3 > $O/shard_emulation_C3.txt 2> $O/shard.err || exit 1
-tail -1 $O/shard_emulation_C3.txt > $O/shard_emulation_C3.json
-timeout -k 10 400 python -u scripts/shard_emulation.py --config C4 > $O/shard_emulation_C4.txt 2>> $O/shard.err || exit 1
-tail -1 $O/shard_emulation_C4.txt > $O/shard_emulation_C4.json
-cat $O/shard_emulation_C3.json $O/shard_emulation_C4.json
+O=gpurun_out/r02y; mkdir -p $O
+for rep in 1 2; do
+  for t in 4096 0; do
+    OCTPT_DRAIN_RAYS=$t timeout -k 10 400 python3 bench.py --config C5 --steps 1 --warmup 1 --no-cpu-baseline > $O/b.json 2>> $O/err || exit 1
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'])" $O/b.json "C5full drain$t" | tee -a $O/ab.txt
+    OCTPT_DRAIN_RAYS=$t timeout -k 10 400 python3 bench.py --config C3 --steps 3 --warmup 1 --no-cpu-baseline > $O/b.json 2>> $O/err || exit 1
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'])" $O/b.json "C3 drain$t" | tee -a $O/ab.txt
+  done
+done

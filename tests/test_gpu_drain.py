@@ -2,8 +2,9 @@
 finishes the queued paths in-lane instead of one extend / shade pair per remaining segment.  It runs
 the wavefront's own per-segment code and record formats, so a render with the drain is bit-identical
 to one without it (OCTPT_DRAIN_RAYS=0): radiance, per-pixel segment counts and every statistic, on
-sphere, box, block-model, sun-sampling and branch-count scenes, and with a pool small enough that
-several chunks each end in a drain."""
+sphere, box, sun-sampling and branch-count scenes, and with a pool small enough that several chunks
+each end in a drain.  Block-model scenes (C5, blocks) keep the tail iterations; their cases check
+that the switch leaves them alone."""
 import os
 
 import numpy as np
