@@ -1,0 +1,79 @@
+"""The measurement plumbing on the CPU: bench.py's algorithmic byte
+counts and traffic loading, and scripts/pmc_traffic.py's per-launch traffic and L2 hit rate from
+rocprofv3 counter CSVs (synthetic files in rocprofv3's column layout)."""
+import csv
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+COLS = ["Correlation_Id", "Dispatch_Id", "Agent_Id", "Queue_Id", "Process_Id", "Thread_Id", "Grid_Size", "Kernel_Id",
+        "Kernel_Name", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count",
+        "Counter_Name", "Counter_Value", "Start_Timestamp", "End_Timestamp"]
+EXT = "void octpt::(anonymous namespace)::wf_extend_kernel<0>(octpt::DevScene, octpt::WaveBuffers, unsigned int, " \
+      "unsigned int, unsigned long long*)"
+SHADE = "void octpt::(anonymous namespace)::wf_shade_kernel<false, true>(octpt::DevScene, ...)"
+
+
+def _csv(d: Path, rows):
+    d.mkdir(parents=True)
+    with open(d / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=COLS)
+        w.writeheader()
+        for i, (kernel, counter, value) in enumerate(rows):
+            r = dict.fromkeys(COLS, 0)
+            r.update(Correlation_Id=i + 1, Dispatch_Id=i + 1, Agent_Id="Agent 2", Kernel_Name=kernel,
+                     Counter_Name=counter, Counter_Value=value)
+            w.writerow(r)
+
+
+def test_pmc_traffic_per_launch_and_l2(tmp_path):
+    # two extend launches and one shade launch; the runtime's own copy kernel is ignored
+    _csv(tmp_path / "fetch", [("__amd_rocclr_copyBuffer", "FETCH_SIZE", 9.0), (EXT, "FETCH_SIZE", 1000.0),
+                              (SHADE, "FETCH_SIZE", 50.0), (EXT, "FETCH_SIZE", 3000.0)])
+    _csv(tmp_path / "write", [(EXT, "WRITE_SIZE", 10.0), (SHADE, "WRITE_SIZE", 20.0), (EXT, "WRITE_SIZE", 30.0)])
+    _csv(tmp_path / "tcc", [(EXT, "TCC_HIT_sum", 90.0), (EXT, "TCC_MISS_sum", 10.0), (EXT, "TCC_HIT_sum", 60.0),
+                            (EXT, "TCC_MISS_sum", 40.0), (SHADE, "TCC_HIT_sum", 1.0), (SHADE, "TCC_MISS_sum", 3.0)])
+    out = tmp_path / "pmc.json"
+    subprocess.run([sys.executable, str(ROOT / "scripts" / "pmc_traffic.py"), str(tmp_path / "fetch"),
+                    str(tmp_path / "write"), "CX", str(out), "1.0", "test", str(tmp_path / "tcc")], check=True,
+                   capture_output=True)
+    d = json.loads(out.read_text())
+    e = d["wf_extend_kernel"]
+    assert e["launches"] == 2
+    assert e["fetch_bytes_per_launch"] == 2000 * 1024 and e["write_bytes_per_launch"] == 20 * 1024
+    assert e["bytes_per_launch"] == 2020 * 1024
+    assert e["l2_hit_rate"] == pytest.approx(150.0 / 200.0)
+    assert d["wf_shade_kernel"]["l2_hit_rate"] == pytest.approx(0.25)
+    assert d["fetch_factor"] == 1.0
+    # the guide's halving (factor 2) doubles the fetch bytes only
+    subprocess.run([sys.executable, str(ROOT / "scripts" / "pmc_traffic.py"), str(tmp_path / "fetch"),
+                    str(tmp_path / "write"), "CX", str(out)], check=True, capture_output=True)
+    e2 = json.loads(out.read_text())["wf_extend_kernel"]
+    assert e2["fetch_bytes_per_launch"] == 2 * e["fetch_bytes_per_launch"] and "l2_hit_rate" not in e2
+
+
+def test_bench_byte_counts():
+    import bench
+
+    st = {"esvo_steps": 1000, "sphere_tests": 10, "cuboid_tests": 5, "segments": 7, "shade_events": 3,
+          "texel_reads": 2, "paths": 4}
+    assert bench.extend_bytes(st) == 8 * 1000 + 20 * 10 + 28 * 5
+    assert bench.extend_queue_bytes(st) == 40 * 7
+    assert bench.shade_bytes(st) == 152 * 7 + 68 * 3 + 4 * 2 + 16 * 4
+
+
+def test_bench_loads_committed_traffic():
+    import bench
+
+    traffic, src, l2 = bench.load_traffic("C3")
+    assert traffic and traffic > 0 and "pmc_C3.json" in src
+    assert l2 is None or 0.0 < l2 < 1.0
+    assert bench.load_traffic("no-such-config") == (None, None, None)
+    h = bench.host_cpu()
+    assert h["threads"] >= 1 and h["affinity"] >= 1 and h["model"]
