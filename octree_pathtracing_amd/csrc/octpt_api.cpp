@@ -624,7 +624,7 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
         ctx->wave_allocs.clear();
         ctx->pool = 0;
         WaveBuffers &B = ctx->wb;
-        // queues + path state (112 B per slot).  When the device cannot hold them (another tenant,
+        // queues + path state (116 B per slot).  When the device cannot hold them (another tenant,
         // the host application's own allocations) the pool is halved down to kMinPool: a smaller
         // pool renders the same frame in more extend launches
         size_t want = pool;
@@ -638,6 +638,7 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
             if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pa);
             if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pb);
             if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pc);
+            if (e == hipSuccess) e = wave_alloc(ctx, want, &B.item0);
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.hit);
             if (e == hipSuccess) e = wave_alloc(ctx, kCtrlWords, &B.ctrl);
             if (e == hipSuccess) break;
@@ -763,7 +764,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, grid_extend, ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
             if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
-            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, grid_shade, ctx->d_stats, s));
+            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, it == 0u, grid_shade, ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 1, ev)) != OCTPT_OK) return st;
             // snapshot of the queue iteration `it` produced; the host checks the snapshot of
             // iteration it - kLookahead, so the GPU always has kLookahead iterations queued (an

@@ -161,6 +161,7 @@ struct WaveBuffers {
     float4 *pa;     // (T.xyz, L.x)
     float4 *pb;     // (L.y, L.z, rng, item)
     uint2 *pc;      // (cur_mat, depth | specular << 8 | path_segs << 16)
+    uint32_t *item0;  // per slot: the chunk item the seed started there (the first shade rebuilds pa / pb / pc)
     uint2 *hit;     // per queue position: (cuboid bit | flags << 27 | prim index, t) -- hit_record()
     float4 *color;  // per chunk item: (L.xyz, path segments)
     // sun-sampling state, 4 planes of `pool` float4:
@@ -196,8 +197,9 @@ hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuff
                           uint32_t chunk_items, unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
                             unsigned long long *stats, hipStream_t stream);
+// first: the chunk's first shade (the seed's rays: path state rebuilt from item0)
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
-                           uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream);
+                           uint32_t chunk_items, bool first, int grid, unsigned long long *stats, hipStream_t stream);
 // the drain of a chunk's last queued rays (every chunk item claimed): one launch, paths finished in-lane
 hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuffers &B, uint32_t q, int grid,
                            unsigned long long *stats, hipStream_t stream);

@@ -1587,11 +1587,19 @@ __device__ __forceinline__ void store_ray(const WaveBuffers &B, uint32_t q, uint
                                  __uint_as_float(slot | (vdot(ps.d, ps.n) < 0.0f ? 0x80000000u : 0u)));
 }
 
+__device__ __forceinline__ void pack_path(const PathState &ps, uint32_t item, float4 &a, float4 &b, uint2 &c) {
+    a = make_float4(ps.T.x, ps.T.y, ps.T.z, ps.L.x);
+    b = make_float4(ps.L.y, ps.L.z, __uint_as_float(ps.rng), __uint_as_float(item));
+    c = make_uint2(ps.cur, ps.depth | (ps.specular ? 1u << 8 : 0u) | (ps.shadow ? 1u << 9 : 0u) | (ps.branch << 10) |
+                               (ps.path_segs << 16) | (ps.seg_base << 23));
+}
 __device__ __forceinline__ void store_path(const WaveBuffers &B, uint32_t slot, const PathState &ps, uint32_t item) {
-    B.pa[slot] = make_float4(ps.T.x, ps.T.y, ps.T.z, ps.L.x);
-    B.pb[slot] = make_float4(ps.L.y, ps.L.z, __uint_as_float(ps.rng), __uint_as_float(item));
-    B.pc[slot] = make_uint2(ps.cur, ps.depth | (ps.specular ? 1u << 8 : 0u) | (ps.shadow ? 1u << 9 : 0u) |
-                                        (ps.branch << 10) | (ps.path_segs << 16) | (ps.seg_base << 23));
+    float4 a, b;
+    uint2 c;
+    pack_path(ps, item, a, b, c);
+    B.pa[slot] = a;
+    B.pb[slot] = b;
+    B.pc[slot] = c;
 }
 
 // sun-sampling state of a slot (kNee): the waiting bounce + mult, and the attenuation
@@ -1614,10 +1622,8 @@ __device__ __forceinline__ void load_nee(const WaveBuffers &B, uint32_t slot, Pa
     ps.att[0] = d.x; ps.att[1] = d.y; ps.att[2] = d.z; ps.att[3] = d.w;
 }
 
-__device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, float4 r0, float4 r1, PathState &ps,
-                                          uint32_t &item) {
-    const float4 a = B.pa[slot], b = B.pb[slot];
-    const uint2 c = B.pc[slot];
+__device__ __forceinline__ void unpack_path(float4 a, float4 b, uint2 c, float4 r0, float4 r1, PathState &ps,
+                                            uint32_t &item) {
     ps.o = V(r0.x, r0.y, r0.z);
     ps.last_prim = __float_as_uint(r0.w);
     ps.d = V(r1.x, r1.y, r1.z);
@@ -1634,17 +1640,17 @@ __device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, f
     ps.path_segs = (c.y >> 16) & 127u;
     ps.seg_base = c.y >> 23;
 }
+__device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, float4 r0, float4 r1, PathState &ps,
+                                          uint32_t &item) {
+    unpack_path(B.pa[slot], B.pb[slot], B.pc[slot], r0, r1, ps, item);
+}
 
-// generate the path of chunk item `item` into `slot`; false when the pixel lies outside the image
-__device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t slot,
-                                 uint32_t item, PathState &ps, Counters &cnt) {
+// the path of chunk item `item`, its first segment begun; false when the pixel lies outside the image
+__device__ __forceinline__ bool item_path(const DevCamera &C, const DevRender &R, uint32_t item, PathState &ps) {
     const uint32_t px_item = item % R.total_items, s_local = item / R.total_items;
     uint32_t x, y;
     item_pixel(R, px_item, x, y);
-    if (x >= R.W || y >= R.H) {
-        B.color[item] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        return false;
-    }
+    if (x >= R.W || y >= R.H) return false;
     uint32_t sample = R.spp_start + s_local, branch = 0u;
     if (R.subs) {  // branch schedule (C20): the pass's sample key and this item's branch
         const uint2 sb = R.subs[s_local];
@@ -1654,8 +1660,22 @@ __device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const W
     new_path(C, R, y * R.W + x, sample, ps);
     ps.branch = branch;
     begin_segment(ps);  // first segment: never capped
+    return true;
+}
+
+// generate the path of chunk item `item` into `slot`; false when the pixel lies outside the image.
+// kSeed (wf_seed_kernel): only the item is stored (item0); the chunk's first shade rebuilds the path
+// state from it (shade_lane) instead of reading 40 B per slot that the seed would have written.
+template <bool kSeed = false>
+__device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t slot,
+                                 uint32_t item, PathState &ps, Counters &cnt) {
+    if (!item_path(C, R, item, ps)) {
+        B.color[item] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        return false;
+    }
     cnt.paths++;
-    store_path(B, slot, ps, item);
+    if (kSeed) B.item0[slot] = item;
+    else store_path(B, slot, ps, item);
     return true;
 }
 
@@ -1686,6 +1706,7 @@ struct ItemCursor {
 // with items left.  Items whose pixel lies outside the image are consumed (zero colour) and the
 // lane draws again, so a slot only goes idle once every shard is exhausted.  Every lane of the
 // wave must call this.
+template <bool kSeed = false>
 __device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t slot, bool want,
                              uint32_t chunk_items, ItemCursor &cur, PathState &ps, Counters &cnt) {
     bool need = want, ok = false;
@@ -1695,7 +1716,7 @@ __device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveB
         bool dry = false;
         if (need) {
             if (t >= n) dry = true;
-            else if (seed_item(C, R, B, slot, lo + t, ps, cnt)) { ok = true; need = false; }
+            else if (seed_item<kSeed>(C, R, B, slot, lo + t, ps, cnt)) { ok = true; need = false; }
         }
         if (__ballot(dry) != 0ull) {
             const uint32_t j = threadIdx.x & 63u;
@@ -1717,7 +1738,7 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     PathState ps;
     ItemCursor cur = {seg, true};
-    const bool ok = regen(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
+    const bool ok = regen<true>(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
     const uint32_t t = wave_ticket(B.ctrl + ctr_count(0u, seg), ok);
     if (ok) store_ray(B, 0u, seg * B.seg_cap + t, i, ps);
     flush_counters(cnt, stats);
@@ -1862,13 +1883,25 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
 // Shade of one traced segment (a lane of wf_shade_kernel, and of wf_drain_kernel): the path in the ray
 // record's slot is loaded, its hit record (hr, extend's output) committed and its shading step taken.
 // Returns true when the path continues (its state stored to the slot, the next ray in ps), false when
-// it finished (its colour record written).
+// it finished (its colour record written).  first (wave-uniform: the chunk's first shade, whose
+// rays the seed started): the path state is rebuilt from the slot's item as the seed computed it,
+// through the same pack / unpack as a stored path, instead of being read.
 template <bool kNee>
-__device__ __forceinline__ bool shade_lane(const DevScene &S, const DevRender &R, const WaveBuffers &B, float4 r0,
-                                           float4 r1, const uint2 *hit_rec, PathState &ps, uint32_t &slot,
-                                           uint32_t &item, Counters &cnt) {
+__device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C, const DevRender &R,
+                                           const WaveBuffers &B, bool first, float4 r0, float4 r1, const uint2 *hit_rec,
+                                           PathState &ps, uint32_t &slot, uint32_t &item, Counters &cnt) {
     slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
-    load_path(B, slot, r0, r1, ps, item);
+    if (first) {
+        item = B.item0[slot];
+        PathState s0;
+        item_path(C, R, item, s0);  // the seed only queued items inside the image
+        float4 a, b;
+        uint2 c;
+        pack_path(s0, item, a, b, c);
+        unpack_path(a, b, c, r0, r1, ps, item);
+    } else {
+        load_path(B, slot, r0, r1, ps, item);
+    }
     const bool was_shadow = kNee && ps.shadow;
     if (was_shadow) load_nee(B, slot, ps);
     const uint2 hr = *hit_rec;
@@ -1913,7 +1946,7 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevRender &R
 constexpr uint32_t kShadeLdsMats = OCTPT_SHADE_LDS_MATS;
 template <bool kNee, bool kLdsMats>
 __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
-                                                          uint32_t q, uint32_t chunk_items,
+                                                          uint32_t q, uint32_t chunk_items, uint32_t first,
                                                           unsigned long long *__restrict__ stats) {
     constexpr uint32_t kT = (kLdsMats && kShadeLdsMats) ? kShadeLdsMats : 1u;
     __shared__ DevMaterial smats[kT];
@@ -1948,7 +1981,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
         PathState ps;
         if (valid) {
             const float4 r0 = B.ray0[q][i], r1 = B.ray1[q][i];
-            append = shade_lane<kNee>(S, R, B, r0, r1, B.hit + i, ps, slot, item, cnt);
+            append = shade_lane<kNee>(S, C, R, B, first != 0u, r0, r1, B.hit + i, ps, slot, item, cnt);
             finished = !append;
         }
         // regenerate: finished lanes take the next chunk items (path regeneration)
@@ -1996,7 +2029,7 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                 const uint2 hr = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
                 PathState ps;
                 uint32_t slot, item;
-                if (!shade_lane<kNee>(S, R, B, r0, r1, &hr, ps, slot, item, cnt)) break;
+                if (!shade_lane<kNee>(S, DevCamera{}, R, B, false, r0, r1, &hr, ps, slot, item, cnt)) break;
                 // the next segment's ray record, as store_ray writes it
                 r0 = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.last_prim));
                 r1 = make_float4(ps.d.x, ps.d.y, ps.d.z,
@@ -2204,11 +2237,12 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
 }
 
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
-                           uint32_t chunk_items, int grid, unsigned long long *stats, hipStream_t stream) {
+                           uint32_t chunk_items, bool first, int grid, unsigned long long *stats, hipStream_t stream) {
     const bool lds = S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats;
     auto kern = S.sun.sun_sampling ? (lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
                                    : (lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, stats);
+    const uint32_t first_u = first ? 1u : 0u;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, first_u, stats);
     return hipGetLastError();
 }
 
