@@ -34,7 +34,7 @@ constexpr uint64_t kMaxChunkPaths = 1ull << 31;    // colour buffer: up to 32 Gi
 constexpr uint64_t kDefaultChunkPaths = 1ull << 29;  // 4K: 64-spp chunks (C5 4634 vs 3882 Mrays/s at 2^30; C3 stays one chunk)
                                                     // (C3 = 530 M paths = one chunk: one drain tail)
 constexpr uint32_t kLookahead = 3;                  // host steering: iterations queued ahead of the check
-constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (57 GB of queues + path state)
+constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (116 B each: queues + path state)
 constexpr uint32_t kMaxPool = 1u << 30;              // the sun-sampling planes index 4 * pool slots in uint32
 constexpr uint32_t kMinPool = 1u << 20;              // floor of the out-of-memory fallback (halving)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
