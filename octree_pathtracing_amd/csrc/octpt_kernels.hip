@@ -1730,15 +1730,24 @@ __device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveB
 }
 
 // seed: slot i starts a path; wave w appends to queue 0 segment w % kSegs, which holds at most
-// seg_cap rays (seg_cap = ceil(ceil(pool / 64) / kSegs) * 64)
+// seg_cap rays (seg_cap = ceil(ceil(pool / 64) / kSegs) * 64).  When the pool holds the whole chunk
+// (n_seed == chunk_items: C3's frame, every 4K chunk) slot i takes item i directly and block 0 marks
+// every shard's items claimed, instead of one item-claim atomic per wave on the 64 shard counters.
 __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender R, WaveBuffers B, uint32_t n_seed,
                                                          uint32_t chunk_items, unsigned long long *__restrict__ stats) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t seg = (i >> 6) % kSegs;
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     PathState ps;
-    ItemCursor cur = {seg, true};
-    const bool ok = regen<true>(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
+    bool ok = false;
+    if (n_seed == chunk_items) {
+        if (blockIdx.x == 0u && threadIdx.x < kSegs)
+            B.ctrl[ctr_item(threadIdx.x)] = shard_lo(threadIdx.x + 1u, chunk_items) - shard_lo(threadIdx.x, chunk_items);
+        if (i < n_seed) ok = seed_item<true>(C, R, B, i, i, ps, cnt);
+    } else {
+        ItemCursor cur = {seg, true};
+        ok = regen<true>(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
+    }
     const uint32_t t = wave_ticket(B.ctrl + ctr_count(0u, seg), ok);
     if (ok) store_ray(B, 0u, seg * B.seg_cap + t, i, ps);
     flush_counters(cnt, stats);
