@@ -1729,10 +1729,14 @@ __device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveB
     return ok;
 }
 
-// seed: slot i starts a path; wave w appends to queue 0 segment w % kSegs, which holds at most
-// seg_cap rays (seg_cap = ceil(ceil(pool / 64) / kSegs) * 64).  When the pool holds the whole chunk
-// (n_seed == chunk_items: C3's frame, every 4K chunk) slot i takes item i directly and block 0 marks
-// every shard's items claimed, instead of one item-claim atomic per wave on the 64 shard counters.
+// seed: wave w appends to queue 0 segment w % kSegs, which holds at most seg_cap rays
+// (seg_cap = ceil(ceil(pool / 64) / kSegs) * 64).  When the pool holds the whole chunk
+// (n_seed == chunk_items: C3's frame, every 4K chunk) the waves of segment k take shard k's items
+// in order, item = slot (no item-claim atomics; block 0 marks every shard claimed; the grid is
+// launch_wf_seed's kSegs * ceil(shard / 64) waves).  Segment k then holds shard k's samples in tile
+// order, so the extend waves draining the 64 segments side by side trace the same image tile for
+// 64 sample groups (the item-claim path's order, whose L2 locality this keeps).  Otherwise slot i
+// claims items from the shards (regen).
 __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender R, WaveBuffers B, uint32_t n_seed,
                                                          uint32_t chunk_items, unsigned long long *__restrict__ stats) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -1740,16 +1744,19 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     PathState ps;
     bool ok = false;
+    uint32_t slot = i;
     if (n_seed == chunk_items) {
         if (blockIdx.x == 0u && threadIdx.x < kSegs)
             B.ctrl[ctr_item(threadIdx.x)] = shard_lo(threadIdx.x + 1u, chunk_items) - shard_lo(threadIdx.x, chunk_items);
-        if (i < n_seed) ok = seed_item<true>(C, R, B, i, i, ps, cnt);
+        const uint32_t item = shard_lo(seg, chunk_items) + (i >> 6) / kSegs * 64u + (i & 63u);
+        slot = item;
+        if (item < shard_lo(seg + 1u, chunk_items)) ok = seed_item<true>(C, R, B, slot, item, ps, cnt);
     } else {
         ItemCursor cur = {seg, true};
         ok = regen<true>(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
     }
     const uint32_t t = wave_ticket(B.ctrl + ctr_count(0u, seg), ok);
-    if (ok) store_ray(B, 0u, seg * B.seg_cap + t, i, ps);
+    if (ok) store_ray(B, 0u, seg * B.seg_cap + t, slot, ps);
     flush_counters(cnt, stats);
 }
 
@@ -2230,7 +2237,11 @@ hipError_t launch_render(const DevScene &S0, const DevCamera &C, const DevRender
 
 hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t n_seed,
                           uint32_t chunk_items, unsigned long long *stats, hipStream_t stream) {
-    hipLaunchKernelGGL(wf_seed_kernel, dim3((n_seed + kBlock - 1u) / kBlock), dim3(kBlock), 0, stream, C, R, B, n_seed,
+    // direct seeding: kSegs segments x ceil(largest shard / 64) waves (each shard <= ceil(n / kSegs))
+    const uint64_t threads = n_seed == chunk_items
+                                 ? (uint64_t)kSegs * ((((uint64_t)chunk_items + kSegs - 1u) / kSegs + 63u) / 64u) * 64u
+                                 : (uint64_t)n_seed;
+    hipLaunchKernelGGL(wf_seed_kernel, dim3((uint32_t)((threads + kBlock - 1u) / kBlock)), dim3(kBlock), 0, stream, C, R, B, n_seed,
                        chunk_items, stats);
     return hipGetLastError();
 }
