@@ -1782,7 +1782,10 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #define OCTPT_EXTEND_WAVES_OF(k) \
     ((k) == kPrimsSpheres ? OCTPT_SPH_WAVES : (k) == kPrimsBoxes ? OCTPT_BOX_WAVES : OCTPT_MDL_WAVES)
 // positions a wave claims from its segment at a time (one atomic per claim)
-constexpr uint32_t kClaim = 64u;
+#ifndef OCTPT_CLAIM
+#define OCTPT_CLAIM 64
+#endif
+constexpr uint32_t kClaim = OCTPT_CLAIM;
 // refill == 0 (adaptive): rays shorter than this many ESVO steps on average refill 32 at a time
 constexpr uint32_t kShortRaySteps = 56u;
 template <int kPrims>
