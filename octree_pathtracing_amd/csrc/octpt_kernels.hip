@@ -1787,6 +1787,12 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #endif
 constexpr uint32_t kClaim = OCTPT_CLAIM;
 // refill == 0 (adaptive): rays shorter than this many ESVO steps on average refill 32 at a time
+#ifndef OCTPT_THR_LONG
+#define OCTPT_THR_LONG 16   // refill threshold of waves with long rays (A/B knob)
+#endif
+#ifndef OCTPT_THR_SHORT
+#define OCTPT_THR_SHORT 32  // ... and with short rays
+#endif
 constexpr uint32_t kShortRaySteps = 56u;
 template <int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
@@ -1824,7 +1830,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
     // out positions without waiting on an atomic's round trip
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t c_next = 0u, c_end = 0u, claim_v = 0u;
-    uint32_t thr = refill ? refill : 16u;  // idle lanes that trigger a refill (wave-uniform)
+    uint32_t thr = refill ? refill : OCTPT_THR_LONG;  // idle lanes that trigger a refill (wave-uniform)
     uint32_t lane_rays = 0u;                // rays this lane started (adaptive threshold)
     if (lane == 0u)
         claim_v = __hip_atomic_fetch_add(B.ctrl + ctr_head(q, seg), kClaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1872,7 +1878,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 // adaptive threshold: when most lanes' rays so far averaged fewer
                 // than kShortRaySteps ESVO steps, the wave refills 32 at a time, else 16
                 const bool short_rays = cnt.steps < kShortRaySteps * lane_rays;
-                thr = __popcll(__ballot(short_rays)) > 32 ? 32u : 16u;
+                thr = __popcll(__ballot(short_rays)) > 32 ? OCTPT_THR_SHORT : OCTPT_THR_LONG;
             }
         }
         // inner loop: step until `thr` lanes are idle (every lane, once no ray is left); its only
