@@ -33,7 +33,10 @@ constexpr uint32_t kCounterRing = 256;
 constexpr uint64_t kMaxChunkPaths = 1ull << 31;    // colour buffer: up to 32 GiB of float4 per chunk (OCTPT_CHUNK)
 constexpr uint64_t kDefaultChunkPaths = 1ull << 29;  // 4K: 64-spp chunks (C5 4634 vs 3882 Mrays/s at 2^30; C3 stays one chunk)
                                                     // (C3 = 530 M paths = one chunk: one drain tail)
-constexpr uint32_t kLookahead = 3;                  // host steering: iterations queued ahead of the check
+#ifndef OCTPT_LOOKAHEAD
+#define OCTPT_LOOKAHEAD 3
+#endif
+constexpr uint32_t kLookahead = OCTPT_LOOKAHEAD;    // host steering: iterations queued ahead of the check
 constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (116 B each: queues + path state)
 constexpr uint32_t kMaxPool = 1u << 30;              // the sun-sampling planes index 4 * pool slots in uint32
 constexpr uint32_t kMinPool = 1u << 20;              // floor of the out-of-memory fallback (halving)
