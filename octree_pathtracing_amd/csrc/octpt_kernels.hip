@@ -1793,7 +1793,10 @@ constexpr uint32_t kClaim = OCTPT_CLAIM;
 #ifndef OCTPT_THR_SHORT
 #define OCTPT_THR_SHORT 32  // ... and with short rays
 #endif
-constexpr uint32_t kShortRaySteps = 56u;
+#ifndef OCTPT_SHORT_STEPS
+#define OCTPT_SHORT_STEPS 56  // mean ESVO steps below which a wave's rays count as short (A/B knob)
+#endif
+constexpr uint32_t kShortRaySteps = OCTPT_SHORT_STEPS;
 template <int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            unsigned long long *__restrict__ stats) {
