@@ -39,17 +39,27 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 METRIC = "Mrays/sec at 1920×1080×256spp; achieved HBM GB/s vs roofline at 1/2/4/8 GPUs"
 
 
+def extend_share(st: dict) -> dict:
+    """The counters of the extend launches: the totals minus the chunk-tail drain kernel's share
+    (octpt_stats.drain; the drain is timed apart, rocprof lists it as wf_drain_kernel)."""
+    d = st.get("drain", {})
+    return {k: st.get(k, 0) - d.get(k, 0) for k in ("segments", "esvo_steps", "sphere_tests", "cuboid_tests",
+                                                      "block_tests", "issued_bytes")}
+
+
 def extend_bytes(st: dict) -> float:
     """SURVEY.md §8(d) for wf_extend_kernel: 8 B per ESVO iteration (one node record:
     child mask + child payload; reference iterations, the folded ones included), 16 + 4 B per sphere
-    test (centre/radius float4 + leaf prim index), 24 + 4 B per cuboid test (min/max + index).  The
-    wavefront's own queue traffic (extend_queue_bytes) is not in §8(d) and is reported beside it."""
-    return 8.0 * st["esvo_steps"] + 20.0 * st["sphere_tests"] + 28.0 * st["cuboid_tests"]
+    test (centre/radius float4 + leaf prim index), 24 + 4 B per cuboid test (min/max + index); a
+    block-value leaf (C23) is the node record alone.  The wavefront's own queue traffic
+    (extend_queue_bytes) is not in §8(d) and is reported beside it.  Drain work excluded."""
+    e = extend_share(st)
+    return 8.0 * e["esvo_steps"] + 20.0 * e["sphere_tests"] + 28.0 * e["cuboid_tests"]
 
 
 def extend_queue_bytes(st: dict) -> float:
     """The wavefront's queue traffic in extend: 32-B ray record read + 8-B hit record write per segment."""
-    return 40.0 * st["segments"]
+    return 40.0 * extend_share(st)["segments"]
 
 
 def shade_bytes(st: dict) -> float:
@@ -104,30 +114,80 @@ def native_oracle():
         return ROOT / "oracle" / "libcpu_ref.so", "-O2 -march=x86-64-v2 -ffp-contract=off (native build failed)"
 
 
+def _cpu_rate(sc, cam, rs, seconds: float, threads: int, rows=None):
+    """Oracle Mrays/s on `threads` threads: 1-spp passes of the frame (or of `rows`) until `seconds` elapse."""
+    from oracle import cpu_ref
+
+    acc = None
+    segs = passes = 0
+    t0 = time.perf_counter()
+    while True:
+        acc, _, st = cpu_ref.render(sc, cam, rs.width, rs.height, 1, spp_start=passes, max_depth=rs.max_depth,
+                                    seed=rs.seed, threads=threads, accum=acc, rows=rows)
+        segs += st["segments"]
+        passes += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return segs / dt / 1e6, passes, segs, dt
+
+
 def cpu_baseline(sc, cam, rs, seconds: float, threads: int | None) -> dict:
-    """Oracle on the host cores: whole 1 spp passes of the full frame until `seconds` elapse."""
+    """The oracle (oracle/cpu_ref.c, -O3 -march=native) on the host: whole 1-spp passes of the full
+    frame on the box's CPU share (OMP_NUM_THREADS; the pool's rule for worker pools), and
+    one thread on a band of rows for the per-core rate.  SURVEY §8(d) asks for all host cores: that
+    figure is the per-core rate times the affinity cores, a linear upper bound stated as such."""
     from oracle import cpu_ref
 
     host = host_cpu()
     n = threads or host["threads"]
     lib_path, flags = native_oracle()
     cpu_ref.load(lib_path)
-    acc = None
-    segs = 0
-    passes = 0
-    t0 = time.perf_counter()
-    while True:
-        acc, _, st = cpu_ref.render(sc, cam, rs.width, rs.height, 1, spp_start=passes, max_depth=rs.max_depth,
-                                    seed=rs.seed, threads=n, accum=acc)
-        segs += st["segments"]
-        passes += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": n, "kind": "port",
+    rate, passes, segs, dt = _cpu_rate(sc, cam, rs, seconds, n)
+    band = (rs.height // 2 - 32, rs.height // 2 + 32)  # the frame's middle 64 rows, one thread
+    rate1, passes1, segs1, dt1 = _cpu_rate(sc, cam, rs, max(seconds / 3.0, 2.0), 1, rows=band)
+    return {"value": round(rate, 3), "unit": "Mrays/s", "cores": n, "kind": "port",
             "sample": f"{passes} full-frame pass(es) of the same workload ({rs.width}x{rs.height}, 1 spp each, "
-                      f"{segs} segments) in {dt:.1f} s",
+                      f"{segs} segments) in {dt:.1f} s on {n} threads; 1 thread: {passes1} pass(es) of rows "
+                      f"{band[0]}-{band[1]} ({segs1} segments) in {dt1:.1f} s",
+            "per_core": round(rate1, 4),
+            "all_cores_linear": {"value": round(rate1 * host["affinity"], 2), "cores": host["affinity"],
+                                 "basis": "per-core rate x affinity cores (linear upper bound, not measured)"},
             "cpu_model": host["model"], "nproc": host["nproc"], "affinity": host["affinity"], "build": flags}
+
+
+def issued_probe(sc, cam, rs, dev_idx: int, ext_s: float):
+    """One render of the same step through the OCTPT_COUNT_ISSUED diagnostic library:
+    the bytes extend actually issues per launch (node slots of the lanes that load one, primitives,
+    quads, alpha texels) and the roofline fraction they give over the timed library's launch time."""
+    lib = ROOT / "octree_pathtracing_amd" / "lib" / "liboctpt_issued.so"
+    if not lib.exists():
+        return None
+    import torch
+    from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
+
+    r = HipRenderer(device=dev_idx, lib_path=str(lib))
+    try:
+        r.set_scene(sc)
+        r.set_camera(cam)
+        r.max_depth, r.seed = rs.max_depth, rs.seed
+        W, H = rs.width, rs.height
+        acc = torch.zeros((shard_pixels(W, H, 0, 1), 4), dtype=torch.float32, device=torch.device("cuda", dev_idx))
+        acc[:, 3] = 1.0
+        r.render_device(r.params(W, H, 0, rs.spp, 0, 1, compact=True, kernel_timing=True), acc.data_ptr(), None,
+                        torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        st = r.stats()
+    finally:
+        r.close()
+    n = max(st["extend_launches"], 1)
+    e = extend_share(st)
+    per_launch = e["issued_bytes"] / n
+    achieved = per_launch / ext_s / 1e9 if ext_s > 0 else 0.0
+    return {"bytes_per_launch": int(per_launch), "achieved": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "launches": st["extend_launches"],
+            "basis": "liboctpt_issued.so (-DOCTPT_COUNT_ISSUED): every load extend issues, summed by the kernel; "
+                     "one render of the same step, divided by the timed library's mean extend launch time"}
 
 
 def main():
@@ -142,6 +202,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: the host's CPU share (host_cpu)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-issued", action="store_true", help="skip the issued-bytes probe (diagnostic library)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: host-staged gather (rehearses N ranks on fewer GPUs); nccl = RCCL over xGMI")
     ap.add_argument("--dump-frame", default=None, help="rank 0 saves the gathered frame (.npy) after the last step")
@@ -242,7 +303,7 @@ def main():
 
     n_ext = max(st["extend_launches"], 1)
     ext_s = st["extend_ms"] / 1e3 / n_ext
-    bytes_per_launch = extend_bytes(st) / n_ext
+    bytes_per_launch = extend_bytes(st) / n_ext  # drain work excluded (extend_share)
     achieved = bytes_per_launch / ext_s / 1e9 if ext_s > 0 else 0.0
     n_sh = max(st["shade_launches"], 1)
     sh_s = st["shade_ms"] / 1e3 / n_sh
@@ -285,7 +346,8 @@ def main():
             "launches": st["extend_launches"],
             "kernel_ms_avg": round(ext_s * 1e3, 4),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "bytes_basis": "SURVEY.md §8(d): 8 B x ESVO iterations + 20 B x sphere tests + 28 B x cuboid tests",
+            "bytes_basis": "SURVEY.md §8(d): 8 B x ESVO iterations + 20 B x sphere tests + 28 B x cuboid tests "
+                           "(block-value leaves: the node record only); drain kernel excluded",
             "queue_bytes_per_launch": int(extend_queue_bytes(st) / n_ext),
             "share_of_gpu_time": round(st["extend_ms"] / max(st["extend_ms"] + st["shade_ms"], 1e-9), 3),
             "shade": {"kernel": "wf_shade_kernel", "launches": st["shade_launches"],
@@ -294,6 +356,8 @@ def main():
         },
         "stats_rank0": {k: v for k, v in st.items() if k != "kernel_ms"},
     }
+    if rank == 0 and world == 1 and not args.no_issued:
+        out["roofline"]["issued"] = issued_probe(sc, cam, rs, dev_idx, ext_s)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sc, cam, rs, args.cpu_seconds, args.cpu_threads)
     else:

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTPT_ABI_VERSION 2u
+#define OCTPT_ABI_VERSION 3u
 
 typedef int32_t octpt_status;
 #define OCTPT_OK 0
@@ -131,9 +131,29 @@ typedef struct octpt_sun {
     float luminosity_pdf; /* Sun::luminosity_pdf, 1/100 in Sun::new (scene/mod.rs:376) */
 } octpt_sun;
 
+/* Block-value leaves: the reference's own leaf form.  Every octree the reference
+ * builds stores a u32 block value in its leaves -- (ChildType::Leaf, value) (new_octree.rs:669),
+ * Lod(section_fill_block) (:727), Lod(data) one or more levels up (:534-537, 586) -- and traverses
+ * such a leaf as the cell itself (octree_traversal.rs:143-214).  With octpt_scene_desc.blocks set, a
+ * leaf payload is an index into this table, at any level:
+ *  - model == OCTPT_MODEL_NONE: the block fills its leaf cell (ResourceModel::SingleBlock, :193-206).
+ *    The face is the cell face the ray enters, the texture coordinates its entry point over the cell
+ *    (:156-190), the material face_material[face]; a texel with alpha <= EPSILON lets the ray through
+ *    (the traversal advances), and a ray that starts inside the cell passes it (t_min == 0, :194);
+ *  - else the block model (C19) drawn at the leaf cell's corner in unit-voxel coordinates
+ *    (ResourceModel::Quad, :207-213).
+ * Face order West(-X), East(+X), Bottom(-Y), Top(+Y), South(+Z), North(-Z) (cuboid.rs:9-29).  32 bytes. */
+typedef struct octpt_block {
+    uint32_t face_material[6];
+    uint32_t model;
+    uint32_t reserved;
+} octpt_block;
+
 /* Scene (src/scene/mod.rs:146-156) flattened: octree + leaf primitive lists + primitive,
  * material and texture tables.  Leaf payload p indexes leaf_first/leaf_count; the prims
- * leaf_prims[first .. first+count) are sphere indices, or cuboid indices | 0x80000000. */
+ * leaf_prims[first .. first+count) are sphere indices, or cuboid indices | 0x80000000.
+ * With `blocks` set the leaf payloads are block ids instead (C23): leaf_*, spheres and cuboids
+ * must then be empty, and block models draw from models / quads. */
 typedef struct octpt_scene_desc {
     uint32_t abi_version; /* = OCTPT_ABI_VERSION */
     const octpt_octant *octants;
@@ -161,6 +181,9 @@ typedef struct octpt_scene_desc {
     uint32_t model_count;
     const octpt_quad *quads;
     uint32_t quad_count;
+    /* block-value leaves (C23): NULL = primitive leaves */
+    const octpt_block *blocks;
+    uint32_t block_count;
 } octpt_scene_desc;
 
 /* renderer::camera::Camera (src/renderer/camera.rs:8-25) */
@@ -193,6 +216,17 @@ typedef struct octpt_render_params {
     uint32_t flags;
 } octpt_render_params;
 
+/* statistics counter order of octpt_stats::drain */
+#define OCTPT_STAT_PATHS 0
+#define OCTPT_STAT_SEGMENTS 1
+#define OCTPT_STAT_ESVO_STEPS 2
+#define OCTPT_STAT_SPHERE_TESTS 3
+#define OCTPT_STAT_CUBOID_TESTS 4
+#define OCTPT_STAT_SHADE_EVENTS 5
+#define OCTPT_STAT_TEXEL_READS 6
+#define OCTPT_STAT_BLOCK_TESTS 7
+#define OCTPT_STAT_ISSUED_BYTES 8
+#define OCTPT_STAT_COUNT 9
 typedef struct octpt_stats {
     uint64_t paths, segments, esvo_steps, sphere_tests, cuboid_tests, shade_events, texel_reads;
     uint64_t launches;
@@ -201,6 +235,16 @@ typedef struct octpt_stats {
     uint64_t extend_launches, shade_launches;
     double extend_ms, shade_ms;
     double build_ms; /* device time (upload excluded) of the last octpt_build_octree_device */
+    uint64_t block_tests;  /* block-value leaf tests */
+    /* bytes of the loads wf_extend_kernel issues (node slots actually loaded, primitives, quads, alpha
+     * texels): counted only by the OCTPT_COUNT_ISSUED diagnostic build of the library, else 0 */
+    uint64_t issued_bytes;
+    /* the chunk-tail drain kernel's share of the counters above, in OCTPT_STAT_* order (included in
+     * the totals; the extend roofline subtracts it) */
+    uint64_t drain[OCTPT_STAT_COUNT];
+    uint64_t pool_slots;  /* path slots held by the wavefront state (after any out-of-memory fallback) */
+    uint64_t chunk_items; /* (pixel, sample) items per chunk held (likewise) */
+    uint64_t wave_allocs; /* wavefront-state (re)allocations since the context was created */
 } octpt_stats;
 
 /* --- library / context ------------------------------------------------------ */
@@ -263,8 +307,8 @@ uint32_t octpt_shard_pixels(uint32_t width, uint32_t height, uint32_t shard_inde
 /* Batch closest-hit query = Scene::hit (scene/mod.rs:172-187) with the octree traversal
  * (octree_traversal.rs:54-302) restored.  rays: n*6 floats (origin, unit direction), host.
  * last_prim / last_normal (nullable): self-intersection key per ray.
- * Outputs (host): t (world, +inf on miss), prim (0xFFFFFFFF on miss), normal n*3 (nullable),
- * esvo steps (nullable). */
+ * Outputs (host): t (world, +inf on miss), prim (0xFFFFFFFF on miss; in a block-value scene, C23, the
+ * block id, or 0x40000000 | quad for a block model's quad), normal n*3 (nullable), esvo steps (nullable). */
 octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *last_prim, const float *last_normal,
                              uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps);
 
@@ -315,8 +359,66 @@ octpt_status octpt_build_octree_ex(const octpt_sphere *spheres, uint32_t sphere_
 octpt_status octpt_build_octree_device_ex(octpt_ctx *ctx, const octpt_sphere *spheres, uint32_t sphere_count,
                                           const octpt_cuboid *cuboids, uint32_t cuboid_count, uint32_t depth,
                                           uint32_t flags, octpt_octree **out);
+/* Block-value octree builder (C23): one block per voxel cell, cells[4k .. 4k+3] = (x, y, z, block id),
+ * x, y, z < 2^depth.  Morton-sorted (new_octree.rs:752-835 order) and emitted in pre-order like
+ * octpt_build_octree; the leaf payloads are the block ids (the view's leaf tables are empty).
+ * OCTPT_BUILD_COMPACT merges eight sibling leaves holding the same block value into one leaf of their
+ * parent, bottom-up at every level: Octant::is_compactable's value equality (new_octree.rs:227-233) as
+ * SectionOctantBuilder / RegionOctreeBuilder apply it (:675-690, 582-587); the root is never merged
+ * away.  Two cells at one position, or a block id >= 2^27, are INVALID_ARG. */
+octpt_status octpt_build_block_octree(const uint32_t *cells, uint32_t cell_count, uint32_t depth, uint32_t flags,
+                                      octpt_octree **out);
 octpt_status octpt_octree_get_view(const octpt_octree *tree, octpt_octree_view *view);
 void octpt_octree_free(octpt_octree *tree);
+
+/* --- the reference's Scene, element by element (the host flattener of INTEGRATION.md §3) ---------
+ * textures::material::Material (src/textures/material.rs:91-101) with its Texture (texture.rs:15-18):
+ * Texture::Color(U8Color) or Texture::Image(RTWImage) as RGBA8 rows (rtw_image.rs:30-36). */
+typedef struct octpt_reference_material {
+    float index_of_refraction, specular, emittance, roughness, metalness;
+    uint32_t material_flags, tint_index;
+    uint32_t texture_kind; /* OCTPT_TEXTURE_COLOR / OCTPT_TEXTURE_IMAGE */
+    uint8_t color[4];
+    uint32_t image_width, image_height;
+    const uint8_t *image_rgba; /* image_width * image_height * 4 bytes, top row first */
+} octpt_reference_material;
+/* geometry::quad::Quad (src/geometry/quad.rs:7-17) field by field: origin, u, v and the texture
+ * ranges are Quad::new's arguments; normal, w and d are what Quad::new derived from them (:90-114) */
+typedef struct octpt_reference_quad {
+    float origin[3], u[3], v[3], w[3], normal[3], d;
+    uint32_t material_id;
+    float texture_u_range[2], texture_v_range[2];
+} octpt_reference_quad;
+/* scene::Scene (src/scene/mod.rs:146-156): the octree as new_octree::Octree holds it (octants_slice,
+ * root, depth; either mask encoding, C21; block-value leaves), Box<[Quad]>, Box<[Material]>, the Sun::new
+ * arguments with the SunSamplingStrategy, emitters_enabled, f_sub_surface -- plus the block table the
+ * host's resource manager resolves block values with (block value -> six face materials or a model;
+ * resource_manager.rs:126-318, out of scope) and its block models over `quads`. */
+typedef struct octpt_reference_scene {
+    const octpt_octant *octants;
+    uint32_t octant_count, root, depth;
+    const octpt_block *blocks;
+    uint32_t block_count;
+    const octpt_block_model *models;
+    uint32_t model_count;
+    const octpt_reference_quad *quads;
+    uint32_t quad_count;
+    const octpt_reference_material *materials;
+    uint32_t material_count;
+    octpt_sun sun;
+    int32_t emitters_enabled;
+    float f_sub_surface;
+} octpt_reference_scene;
+/* Fill an octpt_scene_desc (for octpt_scene_upload) from the reference's Scene.  Material i becomes
+ * octpt_material i with its own texture i (the one-texture-per-material layout GPURenderer uploads,
+ * gpu_renderer.rs:221-307); quads keep Quad::new's arguments (octpt_scene_upload derives normal, w and d
+ * again, in glam's order).  No allocation: the caller provides materials_out / textures_out
+ * (material_count each) and quads_out (quad_count); desc_out points into them and into `ref`'s arrays,
+ * so all of them must outlive the upload.  Host-only, no context.  A material, model or quad index out
+ * of range, an image without pixels, or a quad whose stored normal disagrees with u x v is INVALID_ARG. */
+octpt_status octpt_scene_from_reference(const octpt_reference_scene *ref, octpt_material *materials_out,
+                                        octpt_texture *textures_out, octpt_quad *quads_out,
+                                        octpt_scene_desc *desc_out);
 
 #ifdef __cplusplus
 }

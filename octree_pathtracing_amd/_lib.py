@@ -13,7 +13,7 @@ from pathlib import Path
 LIB_DIR = Path(__file__).resolve().parent / "lib"
 LIB_PATH = LIB_DIR / "liboctpt.so"
 
-OCTPT_ABI_VERSION = 2
+OCTPT_ABI_VERSION = 3
 
 OK = 0
 ERR_INVALID_ARG = 1
@@ -81,6 +81,11 @@ class BlockModel(C.Structure):
 
 
 MODEL_NONE = 0xFFFFFFFF
+
+
+class Block(C.Structure):
+    """octpt_block: a block value's six face materials or its block model."""
+    _fields_ = [("face_material", C.c_uint32 * 6), ("model", C.c_uint32), ("reserved", C.c_uint32)]
 # numpy view of octpt_quad rows (Scene.quads)
 QUAD_DTYPE = [("origin", "<f4", (3,)), ("material", "<u4"), ("u", "<f4", (3,)), ("v", "<f4", (3,)),
               ("texture_u_range", "<f4", (2,)), ("texture_v_range", "<f4", (2,)), ("reserved", "<u4", (2,))]
@@ -118,8 +123,32 @@ class SceneDesc(C.Structure):
         ("materials", C.c_void_p), ("material_count", C.c_uint32), ("textures", C.c_void_p),
         ("texture_count", C.c_uint32), ("sun", Sun), ("emitters_enabled", C.c_int32), ("f_sub_surface", C.c_float),
         ("cuboid_model", C.c_void_p), ("models", C.c_void_p), ("model_count", C.c_uint32), ("quads", C.c_void_p),
-        ("quad_count", C.c_uint32),
+        ("quad_count", C.c_uint32), ("blocks", C.c_void_p), ("block_count", C.c_uint32),
     ]
+
+
+class ReferenceMaterial(C.Structure):
+    """octpt_reference_material: textures::material::Material + its Texture (material.rs:91-101)."""
+    _fields_ = [("index_of_refraction", C.c_float), ("specular", C.c_float), ("emittance", C.c_float),
+                ("roughness", C.c_float), ("metalness", C.c_float), ("material_flags", C.c_uint32),
+                ("tint_index", C.c_uint32), ("texture_kind", C.c_uint32), ("color", C.c_uint8 * 4),
+                ("image_width", C.c_uint32), ("image_height", C.c_uint32), ("image_rgba", C.c_void_p)]
+
+
+class ReferenceQuad(C.Structure):
+    """octpt_reference_quad: geometry::quad::Quad field by field (quad.rs:7-17)."""
+    _fields_ = [("origin", C.c_float * 3), ("u", C.c_float * 3), ("v", C.c_float * 3), ("w", C.c_float * 3),
+                ("normal", C.c_float * 3), ("d", C.c_float), ("material_id", C.c_uint32),
+                ("texture_u_range", C.c_float * 2), ("texture_v_range", C.c_float * 2)]
+
+
+class ReferenceScene(C.Structure):
+    """octpt_reference_scene: scene::Scene (scene/mod.rs:146-156) + the host's block table."""
+    _fields_ = [("octants", C.c_void_p), ("octant_count", C.c_uint32), ("root", C.c_uint32), ("depth", C.c_uint32),
+                ("blocks", C.c_void_p), ("block_count", C.c_uint32), ("models", C.c_void_p),
+                ("model_count", C.c_uint32), ("quads", C.c_void_p), ("quad_count", C.c_uint32),
+                ("materials", C.c_void_p), ("material_count", C.c_uint32), ("sun", Sun),
+                ("emitters_enabled", C.c_int32), ("f_sub_surface", C.c_float)]
 
 
 class Camera(C.Structure):
@@ -133,15 +162,25 @@ class RenderParams(C.Structure):
                 ("shard_index", C.c_uint32), ("shard_count", C.c_uint32), ("flags", C.c_uint32)]
 
 
+# octpt_stats::drain order (OCTPT_STAT_*)
+STAT_NAMES = ("paths", "segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events", "texel_reads",
+              "block_tests", "issued_bytes")
+STAT_COUNT = len(STAT_NAMES)
+
+
 class Stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("esvo_steps", C.c_uint64),
                 ("sphere_tests", C.c_uint64), ("cuboid_tests", C.c_uint64), ("shade_events", C.c_uint64),
                 ("texel_reads", C.c_uint64), ("launches", C.c_uint64), ("kernel_ms", C.c_double),
                 ("extend_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("extend_ms", C.c_double),
-                ("shade_ms", C.c_double), ("build_ms", C.c_double)]
+                ("shade_ms", C.c_double), ("build_ms", C.c_double), ("block_tests", C.c_uint64),
+                ("issued_bytes", C.c_uint64), ("drain", C.c_uint64 * STAT_COUNT), ("pool_slots", C.c_uint64),
+                ("chunk_items", C.c_uint64), ("wave_allocs", C.c_uint64)]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        d = {name: getattr(self, name) for name, _ in self._fields_}
+        d["drain"] = dict(zip(STAT_NAMES, list(self.drain)))  # the drain kernel's share (in the totals)
+        return d
 
 
 class OctreeView(C.Structure):
@@ -180,6 +219,8 @@ SIGNATURES = {
     "octpt_build_octree_device": (_i32, [_vp, _vp, _u32, _vp, _u32, _u32, C.POINTER(_vp)]),
     "octpt_build_octree_ex": (_i32, [_vp, _u32, _vp, _u32, _u32, _u32, C.POINTER(_vp)]),
     "octpt_build_octree_device_ex": (_i32, [_vp, _vp, _u32, _vp, _u32, _u32, _u32, C.POINTER(_vp)]),
+    "octpt_build_block_octree": (_i32, [_vp, _u32, _u32, _u32, C.POINTER(_vp)]),
+    "octpt_scene_from_reference": (_i32, [C.POINTER(ReferenceScene), _vp, _vp, _vp, C.POINTER(SceneDesc)]),
     "octpt_octree_get_view": (_i32, [_vp, C.POINTER(OctreeView)]),
     "octpt_octree_free": (None, [_vp]),
 }

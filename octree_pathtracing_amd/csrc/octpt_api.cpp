@@ -21,10 +21,6 @@
 #include "octpt_internal.h"
 #include "octpt_mask.h"
 
-#ifndef OCTPT_NODE_CACHE
-#define OCTPT_NODE_CACHE 0  // see octpt_kernels.hip
-#endif
-
 using namespace octpt;
 
 namespace {
@@ -86,8 +82,6 @@ struct octpt_ctx {
     unsigned long long *d_stats = nullptr;
     uint8_t *d_lut_byte = nullptr;
     float *d_lut_float = nullptr;
-    uint4 *d_chain = nullptr;   // start chain of the camera centre ray (DevScene::chain), per render
-    bool start_chain = true;    // OCTPT_START_CHAIN=0 disables the replay (A/B)
     std::vector<EventPair> pending;
     double kernel_ms = 0.0;
     uint64_t launches = 0;
@@ -100,13 +94,20 @@ struct octpt_ctx {
     float build_ms = 0.0f;  // device time of the last octpt_build_octree_device
     BuildScratch build_scratch;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
-    int extend_bpc_cache[kMaxDepth + 1][3] = {};  // [depth][kPrims]
+    int extend_bpc_cache[kMaxDepth + 1][4] = {};  // [depth][kPrims]
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
     size_t pool = 0, color_cap = 0, nee_pool = 0;  // nee_pool: slots of the sun-sampling planes (wb.pd)
     void *nee_alloc = nullptr;
     std::vector<void *> wave_allocs;
     void *color_alloc = nullptr;
+    // device bytes of the wavefront state (queues, path state, colour records, sun-sampling planes),
+    // tracked against mem_limit (OCTPT_DEVICE_MEM_LIMIT, MiB, 0 = none: a test hook that makes the
+    // out-of-memory fallback reproducible on an idle GPU)
+    size_t wave_bytes = 0, mem_limit = 0;
+    std::vector<std::pair<void *, size_t>> wave_sizes;
+    uint64_t wave_allocs_n = 0;  // successful (re)allocations of the queues + path state
+    bool oom_warned = false;
     uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
     hipEvent_t count_ev[kLookahead + 1] = {};
     uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
@@ -308,6 +309,17 @@ octpt_status validate_head(octpt_ctx *ctx, const octpt_scene_desc *d, bool with_
         return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^27 - 1 spheres or cuboids");
     if (d->sphere_count && !d->spheres) return fail(ctx, OCTPT_ERR_INVALID_ARG, "spheres is NULL");
     if (d->cuboid_count && !d->cuboids) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboids is NULL");
+    if (d->blocks) {  // block-value leaves (C23): the payloads are block ids, there are no primitives
+        if (!with_octree) return fail(ctx, OCTPT_ERR_INVALID_ARG, "a block-value scene is uploaded with its octree");
+        if (d->block_count == 0) return fail(ctx, OCTPT_ERR_INVALID_ARG, "block table is empty");
+        if (d->block_count > kPrimIndexMask + 1u) return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^27 blocks");
+        if (d->leaf_first || d->leaf_count || d->leaf_table_size || d->leaf_prims || d->leaf_prim_count ||
+            d->sphere_count || d->cuboid_count || d->cuboid_model)
+            return fail(ctx, OCTPT_ERR_INVALID_ARG,
+                        "a block-value scene has no leaf primitive lists, spheres, cuboids or cuboid models");
+    } else if (d->block_count) {
+        return fail(ctx, OCTPT_ERR_INVALID_ARG, "block_count without blocks");
+    }
     return OCTPT_OK;
 }
 
@@ -323,10 +335,10 @@ octpt_status validate_scene(octpt_ctx *ctx, const octpt_scene_desc *d, std::vect
         for (int i = 0; i < 8; ++i) {
             const bool present = (m >> i) & 1, leaf = (m >> (i + 8)) & 1;
             if (!present) continue;
-            if (leaf && o.children[i] >= d->leaf_table_size)
+            if (leaf && o.children[i] >= (d->blocks ? d->block_count : d->leaf_table_size))
                 return fail(ctx, OCTPT_ERR_INVALID_ARG, "octant " + std::to_string(n) + " child " + std::to_string(i) +
-                                                            ": leaf payload " + std::to_string(o.children[i]) +
-                                                            " out of range");
+                                                            (d->blocks ? ": block " : ": leaf payload ") +
+                                                            std::to_string(o.children[i]) + " out of range");
             if (!leaf && o.children[i] >= d->octant_count)
                 return fail(ctx, OCTPT_ERR_INVALID_ARG, "octant " + std::to_string(n) + " child " + std::to_string(i) +
                                                             ": child octant index " + std::to_string(o.children[i]) +
@@ -359,12 +371,25 @@ octpt_status validate_tables(octpt_ctx *ctx, const octpt_scene_desc *d) {
         for (int f = 0; f < 6; ++f)
             if (d->cuboids[c].face_material[f] >= d->material_count)
                 return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboid material out of range");
-    // block models (C19)
-    if (d->cuboid_model) {
+    // block-value leaves (C23)
+    for (uint32_t b = 0; d->blocks && b < d->block_count; ++b) {
+        const octpt_block &x = d->blocks[b];
+        if (x.model != OCTPT_MODEL_NONE) {
+            if (x.model >= d->model_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "block model index out of range");
+        } else {
+            for (int f = 0; f < 6; ++f)
+                if (x.face_material[f] >= d->material_count)
+                    return fail(ctx, OCTPT_ERR_INVALID_ARG, "block face material out of range");
+        }
+    }
+    if (d->blocks && d->quad_count > kPrimIndexMask)  // a quad hit record is kPrimCuboidBit | quad (C23)
+        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^27 quads in a block-value scene");
+    // block models (C19; and of block-value scenes, C23)
+    if (d->cuboid_model || d->blocks) {
         if (d->model_count && !d->models) return fail(ctx, OCTPT_ERR_INVALID_ARG, "models is NULL");
         if (d->quad_count && !d->quads) return fail(ctx, OCTPT_ERR_INVALID_ARG, "quads is NULL");
         if (d->quad_count >= kQuadKey) return fail(ctx, OCTPT_ERR_UNSUPPORTED, "more than 2^30 - 1 quads");
-        for (uint32_t c = 0; c < d->cuboid_count; ++c) {
+        for (uint32_t c = 0; d->cuboid_model && c < d->cuboid_count; ++c) {
             const uint32_t m = d->cuboid_model[c];
             if (m == OCTPT_MODEL_NONE) continue;
             if (m >= d->model_count) return fail(ctx, OCTPT_ERR_INVALID_ARG, "cuboid model index out of range");
@@ -431,9 +456,11 @@ octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_
         S.cub_mat = d_cmat;
     }
     // block models (C19): Quad::new (quad.rs:90-114) in glam's f32 operation order
-    bool has_models = false;
+    bool has_models = false;  // the scene draws block models (from cuboids, C19, or from blocks, C23)
     if (d->cuboid_model)
         for (uint32_t c = 0; c < d->cuboid_count && !has_models; ++c) has_models = d->cuboid_model[c] != OCTPT_MODEL_NONE;
+    for (uint32_t b = 0; d->blocks && b < d->block_count && !has_models; ++b)
+        has_models = d->blocks[b].model != OCTPT_MODEL_NONE;
     std::vector<DevQuad> quads;
     std::vector<uint2> models;
     if (has_models) {
@@ -491,9 +518,19 @@ octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_
     uint2 *d_models = nullptr;
     DevQuad *d_quads = nullptr;
     if (has_models) {
-        HIP_TRY(ctx, upload(ctx, d->cuboid_model, d->cuboid_count, &d_cmodel));
+        if (d->cuboid_model) HIP_TRY(ctx, upload(ctx, d->cuboid_model, d->cuboid_count, &d_cmodel));
         HIP_TRY(ctx, upload(ctx, models.data(), models.size(), &d_models));
         HIP_TRY(ctx, upload(ctx, quads.data(), quads.size(), &d_quads));
+    }
+    uint32_t *d_blk_mat = nullptr, *d_blk_model = nullptr;
+    if (d->blocks) {  // C23: six face materials and the model of every block
+        std::vector<uint32_t> bm((size_t)d->block_count * 6), bmod(d->block_count);
+        for (uint32_t b = 0; b < d->block_count; ++b) {
+            std::memcpy(&bm[(size_t)b * 6], d->blocks[b].face_material, 24);
+            bmod[b] = d->blocks[b].model;
+        }
+        HIP_TRY(ctx, upload(ctx, bm.data(), bm.size(), &d_blk_mat));
+        HIP_TRY(ctx, upload(ctx, bmod.data(), bmod.size(), &d_blk_model));
     }
     S.depth = d->depth;
     S.has_cuboids = d->cuboid_count ? 1u : 0u;
@@ -502,18 +539,55 @@ octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_
     S.cub_model = d_cmodel;
     S.models = d_models;
     S.quads = d_quads;
-    S.has_models = has_models ? 1u : 0u;
+    // the cuboid-model path (C19) of the primitive kernels; block-value scenes draw their models in
+    // the block instance (has_blocks)
+    S.has_models = (has_models && !d->blocks) ? 1u : 0u;
+    S.has_blocks = d->blocks ? 1u : 0u;
+    S.blk_mat = d_blk_mat;
+    S.blk_model = d_blk_model;
     S.mats = d_mats;
     S.n_mats = d->material_count;
     S.texs = d_texs;
     S.n_texs = d->texture_count;
     S.texels = d_texels;
     S.lut_float = ctx->d_lut_float;
-    S.chain = ctx->d_chain;
     make_sun(d->sun, lf, S.sun);
     S.sun.f_sub_surface = d->f_sub_surface;
     S.emitters = d->emitters_enabled ? 1 : 0;
     return OCTPT_OK;
+}
+
+// The slot flags of every block (C23, kBlock* in octpt_internal.h): kBlockIsModel for a block model, else
+// bit f for a face whose material's texture holds a texel of alpha byte 0 -- the only texels that
+// SingleBlockModel::intersect's alpha test (texel alpha <= EPSILON, C23) rejects -- so that the leaf test
+// reads a texel only where it can decide something
+std::vector<uint32_t> block_slot_flags(const octpt_scene_desc *d) {
+    std::vector<int8_t> tex_zero(d->texture_count, -1);
+    auto zero_alpha = [&](uint32_t t) {
+        if (tex_zero[t] < 0) {
+            const octpt_texture &x = d->textures[t];
+            bool z = false;
+            if (x.kind == OCTPT_TEXTURE_COLOR) {
+                z = x.rgba[3] == 0;
+            } else {
+                const size_t n = (size_t)x.width * x.height;
+                for (size_t k = 0; k < n && !z; ++k) z = x.pixels[4 * k + 3] == 0;
+            }
+            tex_zero[t] = z ? 1 : 0;
+        }
+        return tex_zero[t] != 0;
+    };
+    std::vector<uint32_t> flags(d->block_count, 0u);
+    for (uint32_t b = 0; b < d->block_count; ++b) {
+        const octpt_block &x = d->blocks[b];
+        if (x.model != OCTPT_MODEL_NONE) {
+            flags[b] = kBlockIsModel;
+            continue;
+        }
+        for (uint32_t f = 0; f < 6; ++f)
+            if (zero_alpha(d->materials[x.face_material[f]].texture_index)) flags[b] |= 1u << f;
+    }
+    return flags;
 }
 
 uint32_t tiles_of_shard(uint32_t n_tiles, uint32_t shard, uint32_t count) {
@@ -587,13 +661,39 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
 
 size_t accum_pixels(const DevRender &R) { return R.compact ? (size_t)R.total_items : (size_t)R.W * R.H; }
 
-void free_wave(octpt_ctx *ctx) {
-    for (void *p : ctx->wave_allocs) (void)hipFree(p);
+// wavefront-state allocations, counted against the optional mem_limit
+hipError_t wave_malloc(octpt_ctx *ctx, void **p, size_t bytes) {
+    *p = nullptr;
+    if (ctx->mem_limit && ctx->wave_bytes + bytes > ctx->mem_limit) return hipErrorOutOfMemory;
+    const hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return e;
+    ctx->wave_bytes += bytes;
+    ctx->wave_sizes.emplace_back(*p, bytes);
+    return hipSuccess;
+}
+void wave_free(octpt_ctx *ctx, void *&p) {
+    if (!p) return;
+    for (size_t i = 0; i < ctx->wave_sizes.size(); ++i)
+        if (ctx->wave_sizes[i].first == p) {
+            ctx->wave_bytes -= ctx->wave_sizes[i].second;
+            ctx->wave_sizes.erase(ctx->wave_sizes.begin() + (ptrdiff_t)i);
+            break;
+        }
+    (void)hipFree(p);
+    p = nullptr;
+}
+// the queues and path state (ctx->wave_allocs)
+void free_queues(octpt_ctx *ctx) {
+    for (void *p : ctx->wave_allocs) wave_free(ctx, p);
     ctx->wave_allocs.clear();
-    if (ctx->color_alloc) (void)hipFree(ctx->color_alloc);
-    ctx->color_alloc = nullptr;
-    if (ctx->nee_alloc) (void)hipFree(ctx->nee_alloc);
-    ctx->nee_alloc = nullptr;
+    ctx->pool = 0;
+    ctx->wb.huv = nullptr;  // allocated with the queues (block-value scenes)
+}
+
+void free_wave(octpt_ctx *ctx) {
+    free_queues(ctx);
+    wave_free(ctx, ctx->color_alloc);
+    wave_free(ctx, ctx->nee_alloc);
     ctx->pool = ctx->color_cap = ctx->nee_pool = 0;
     ctx->wb = WaveBuffers{};
 }
@@ -601,21 +701,32 @@ void free_wave(octpt_ctx *ctx) {
 template <class T>
 hipError_t wave_alloc(octpt_ctx *ctx, size_t n, T **out) {
     void *p = nullptr;
-    const hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
+    const hipError_t e = wave_malloc(ctx, &p, std::max<size_t>(n, 1) * sizeof(T));
     if (e != hipSuccess) return e;
     ctx->wave_allocs.push_back(p);
     *out = static_cast<T *>(p);
     return hipSuccess;
 }
 
-// host snapshot of the iteration's counters: the whole ctrl block (80 KB: queue counts and heads,
-// chunk item claims), read kLookahead iterations later
-constexpr uint32_t kCountSpan = kCtrlWords;
+// host snapshot of the iteration's counters, read kLookahead iterations later: the kSegs segment counts
+// of the queue the iteration's shade filled, then the kSegs chunk item claims (two strided copies of one
+// word per 256-B counter line, not the whole 80-KB ctrl block)
+constexpr uint32_t kCountSpan = 2u * kSegs;
 
 // queue segment capacity: seed wave w fills segment w % kSegs, so ceil(ceil(pool / 64) / kSegs) waves
 size_t seg_cap_for(size_t pool) { return ((pool + 63) / 64 + kSegs - 1) / kSegs * 64; }
 
-octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool nee) {
+// which allocation of ensure_wave ran out of device memory
+enum OomPart { kOomNone = 0, kOomQueues, kOomColor, kOomNee };
+
+// The wavefront state of a render: `pool` path slots of queues + path state, `color_items` colour
+// records, and (nee) the sun-sampling planes of every slot.  Grow-only.  When the queues + path state
+// do not fit (another tenant, the host application's own allocations) the pool halves down to kMinPool
+// and the pool obtained becomes the context's cap (pool_cap), so later renders neither retry the larger
+// pool nor re-allocate.  A colour or sun-sampling allocation that fails returns OOM with *part set; the
+// caller shrinks the chunk or the pool and calls again (enqueue_wavefront).
+octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool nee, bool blocks, OomPart *part) {
+    *part = kOomNone;
     if (!ctx->h_count) {
         HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), (kLookahead + 1) * kCountSpan * sizeof(uint32_t),
                                    hipHostMallocDefault));
@@ -623,13 +734,9 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
     }
     if (pool > ctx->pool) {
         HIP_TRY(ctx, hipDeviceSynchronize());
-        for (void *p : ctx->wave_allocs) (void)hipFree(p);
-        ctx->wave_allocs.clear();
-        ctx->pool = 0;
+        free_queues(ctx);
         WaveBuffers &B = ctx->wb;
-        // queues + path state (116 B per slot).  When the device cannot hold them (another tenant,
-        // the host application's own allocations) the pool is halved down to kMinPool: a smaller
-        // pool renders the same frame in more extend launches
+        // queues + path state: 116 B per slot
         size_t want = pool;
         for (;;) {
             B.seg_cap = (uint32_t)seg_cap_for(want);
@@ -645,36 +752,60 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.hit);
             if (e == hipSuccess) e = wave_alloc(ctx, kCtrlWords, &B.ctrl);
             if (e == hipSuccess) break;
-            for (void *p : ctx->wave_allocs) (void)hipFree(p);
-            ctx->wave_allocs.clear();
+            free_queues(ctx);
             (void)hipGetLastError();
-            if (e != hipErrorOutOfMemory || want <= kMinPool) return hip_fail(ctx, e, "wave buffers");
+            if (e != hipErrorOutOfMemory || want <= kMinPool) {
+                *part = kOomQueues;
+                return hip_fail(ctx, e, "wave buffers");
+            }
             want = std::max<size_t>(want / 2, kMinPool);
         }
-        if (want < pool)
-            std::fprintf(stderr, "octpt: %zu path slots did not fit in device memory; using %zu\n", pool, want);
+        if (want < pool) {
+            if (!ctx->oom_warned)
+                std::fprintf(stderr, "octpt: %zu path slots did not fit in device memory; using %zu\n", pool, want);
+            ctx->oom_warned = true;
+            ctx->pool_cap = (uint32_t)want;  // sticky: later renders ask for at most what fitted
+        }
         B.pool = (uint32_t)want;
         ctx->pool = want;
+        ctx->wave_allocs_n++;
     }
-    if (color_items > ctx->color_cap) {
-        HIP_TRY(ctx, hipDeviceSynchronize());
-        if (ctx->color_alloc) (void)hipFree(ctx->color_alloc);
-        ctx->color_alloc = nullptr;
-        ctx->color_cap = 0;
-        HIP_TRY(ctx, hipMalloc(&ctx->color_alloc, color_items * sizeof(float4)));
-        ctx->color_cap = color_items;
+    // block-value scenes (C23): the hit records' (u, v), one per queue position, with the queues
+    if (blocks && !ctx->wb.huv) {
+        const hipError_t e = wave_alloc(ctx, (size_t)kSegs * ctx->wb.seg_cap, &ctx->wb.huv);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            *part = kOomNee;  // a per-slot plane like the sun-sampling ones: the pool shrinks
+            return hip_fail(ctx, e, "block hit coordinates");
+        }
     }
-    ctx->wb.color = static_cast<float4 *>(ctx->color_alloc);
     // sun-sampling planes (4 x 16 B per slot) only for scenes that sample the sun (C18)
     if (nee && ctx->nee_pool < ctx->pool) {
         HIP_TRY(ctx, hipDeviceSynchronize());
-        if (ctx->nee_alloc) (void)hipFree(ctx->nee_alloc);
-        ctx->nee_alloc = nullptr;
+        wave_free(ctx, ctx->nee_alloc);
         ctx->nee_pool = 0;
-        HIP_TRY(ctx, hipMalloc(&ctx->nee_alloc, 4 * ctx->pool * sizeof(float4)));
+        const hipError_t e = wave_malloc(ctx, &ctx->nee_alloc, 4 * ctx->pool * sizeof(float4));
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            *part = kOomNee;
+            return hip_fail(ctx, e, "sun-sampling planes");
+        }
         ctx->nee_pool = ctx->pool;
     }
     ctx->wb.pd = static_cast<float4 *>(ctx->nee_alloc);
+    if (color_items > ctx->color_cap) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        wave_free(ctx, ctx->color_alloc);
+        ctx->color_cap = 0;
+        const hipError_t e = wave_malloc(ctx, &ctx->color_alloc, color_items * sizeof(float4));
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            *part = kOomColor;
+            return hip_fail(ctx, e, "colour records");
+        }
+        ctx->color_cap = color_items;
+    }
+    ctx->wb.color = static_cast<float4 *>(ctx->color_alloc);
     ctx->wb.pool = (uint32_t)ctx->pool;
     return OCTPT_OK;
 }
@@ -718,18 +849,45 @@ octpt_status enqueue_megakernel(octpt_ctx *ctx, const DevRender &R, float4 *d_ac
 octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_accum, uint32_t *d_seg, hipStream_t s,
                                const std::atomic<bool> *cancel) {
     const uint64_t n_px = R.total_items;
-    uint32_t chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, ctx->chunk_cap / n_px));
-    // a branch-schedule chunk holds whole passes (<= 64 sub-samples each, C20)
-    if (R.subs) chunk_spp = std::max(chunk_spp, std::min(64u, R.spp_count));
-    const uint64_t chunk_max = (uint64_t)chunk_spp * n_px;
-    if (chunk_max > kMaxChunkPaths)  // a branch pass of 64 sub-samples over > 2^25 pixels
-        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "a branch-schedule pass exceeds the 2^31-item chunk limit");
-    octpt_status st = ensure_wave(ctx, (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max), chunk_max,
-                                  ctx->S.sun.sun_sampling != 0);
-    if (st != OCTPT_OK) return st;
+    uint32_t chunk_spp = 1;
+    uint64_t chunk_max = 0;
+    octpt_status st = OCTPT_OK;
+    for (;;) {
+        chunk_spp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(R.spp_count, ctx->chunk_cap / n_px));
+        // a branch-schedule chunk holds whole passes (<= 64 sub-samples each, C20)
+        if (R.subs) chunk_spp = std::max(chunk_spp, std::min(64u, R.spp_count));
+        chunk_max = (uint64_t)chunk_spp * n_px;
+        if (chunk_max > kMaxChunkPaths)  // a branch pass of 64 sub-samples over > 2^25 pixels
+            return fail(ctx, OCTPT_ERR_UNSUPPORTED, "a branch-schedule pass exceeds the 2^31-item chunk limit");
+        OomPart part = kOomNone;
+        st = ensure_wave(ctx, (size_t)std::min<uint64_t>(ctx->pool_cap, chunk_max), chunk_max,
+                         ctx->S.sun.sun_sampling != 0, ctx->S.has_blocks != 0, &part);
+        if (st == OCTPT_OK) break;
+        if (st != OCTPT_ERR_OOM) return st;
+        // out of device memory past the queues: a smaller chunk (colour records) or pool (planes), kept
+        // for later renders; chunks and pools of any size render the same frame
+        if (part == kOomColor && chunk_spp > 1 && !R.subs) {
+            ctx->chunk_cap = (uint64_t)(chunk_spp / 2) * n_px;
+            if (ctx->pool > ctx->chunk_cap) {  // release the queues too: they were sized for the larger chunk
+                HIP_TRY(ctx, hipDeviceSynchronize());
+                free_queues(ctx);
+                ctx->pool_cap = (uint32_t)std::max<uint64_t>(kMinPool, std::min<uint64_t>(ctx->pool_cap, ctx->chunk_cap));
+            }
+        } else if (part == kOomNee && ctx->pool > kMinPool) {
+            HIP_TRY(ctx, hipDeviceSynchronize());
+            ctx->pool_cap = (uint32_t)std::max<size_t>(kMinPool, ctx->pool / 2);
+            free_queues(ctx);
+        } else {
+            return st;
+        }
+        if (!ctx->oom_warned)
+            std::fprintf(stderr, "octpt: wavefront state did not fit in device memory; chunk %llu items, pool cap %u\n",
+                         (unsigned long long)ctx->chunk_cap, ctx->pool_cap);
+        ctx->oom_warned = true;
+    }
     // the pool actually held (smaller than asked after an out-of-memory fallback)
     const size_t pool = (size_t)std::min<uint64_t>(std::min<uint64_t>(ctx->pool_cap, chunk_max), ctx->pool);
-    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)];
+    int &bpc = ctx->extend_bpc_cache[ctx->S.depth][ctx->S.has_blocks ? 3 : ctx->S.has_models ? 2 : (ctx->S.has_cuboids ? 1 : 0)];
     if (bpc == 0) bpc = extend_blocks_per_cu(ctx->S);
     const int grid_extend = ctx->num_cu * bpc;
     if (std::getenv("OCTPT_DEBUG"))
@@ -774,16 +932,18 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             // iteration over an empty queue exits at once).  The queue only empties once every
             // chunk item is claimed: finished paths regenerate in the same shade pass.
             const uint32_t slot = it % (kLookahead + 1);
-            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_count + slot * kCountSpan, B.ctrl, kCountSpan * sizeof(uint32_t),
-                                        hipMemcpyDeviceToHost, s));
+            uint32_t *hs = ctx->h_count + slot * kCountSpan;
+            HIP_TRY(ctx, hipMemcpy2DAsync(hs, sizeof(uint32_t), B.ctrl + ctr_count(q ^ 1u, 0), kCtrStride * sizeof(uint32_t),
+                                          sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, s));
+            HIP_TRY(ctx, hipMemcpy2DAsync(hs + kSegs, sizeof(uint32_t), B.ctrl + ctr_item(0), kCtrStride * sizeof(uint32_t),
+                                          sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, s));
             HIP_TRY(ctx, hipEventRecord(ctx->count_ev[slot], s));
             if (it >= kLookahead) {
                 const uint32_t old = (it - kLookahead) % (kLookahead + 1);
                 HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[old]));
-                const uint32_t *h = ctx->h_count + old * kCountSpan;
-                const uint32_t q_old = ((it - kLookahead) & 1u) ^ 1u;  // the queue that iteration's shade filled
+                const uint32_t *h = ctx->h_count + old * kCountSpan;  // that iteration's shade's queue, items
                 uint64_t queued = 0;
-                for (uint32_t k = 0; k < kSegs; ++k) queued += h[ctr_count(q_old, k)];
+                for (uint32_t k = 0; k < kSegs; ++k) queued += h[k];
                 if (queued == 0u) break;  // iteration it - kLookahead + 1 onwards had nothing to do
                 // Drain: every chunk item claimed and few rays left, so the queue only shrinks from
                 // here (a ray yields at most one ray, and nothing regenerates).  One launch finishes the
@@ -796,7 +956,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
                     for (uint32_t k = 0; k < kSegs && exhausted; ++k) {
                         const uint32_t lo = (uint32_t)(((uint64_t)k * chunk_items) / kSegs);
                         const uint32_t hi = (uint32_t)(((uint64_t)(k + 1u) * chunk_items) / kSegs);
-                        exhausted = h[ctr_item(k)] >= hi - lo;
+                        exhausted = h[kSegs + k] >= hi - lo;
                     }
                     if (exhausted) {
                         // one path per wave (wf_drain_kernel), four waves per block
@@ -822,10 +982,6 @@ octpt_status enqueue_render(octpt_ctx *ctx, const DevRender &R, float4 *d_accum,
     ctx->pending.push_back(ev);  // destroyed by get_stats / destroy
     HIP_TRY(ctx, hipEventRecord(ev.start, s));
     octpt_status st = OCTPT_OK;
-    if (OCTPT_START_CHAIN && !megakernel) {  // the start chain of this camera (extend and preview replay it)
-        if (ctx->start_chain) HIP_TRY(ctx, launch_start_chain(ctx->S, ctx->C, ctx->d_chain, s));
-        else HIP_TRY(ctx, hipMemsetAsync(ctx->d_chain, 0, sizeof(uint4), s));
-    }
     if (R.preview) {
         const hipError_t e = launch_preview(ctx->S, ctx->C, R, d_accum, d_seg, ctx->d_stats, s);
         if (e != hipSuccess) st = hip_fail(ctx, e, "preview launch");
@@ -932,6 +1088,50 @@ struct Builder {
     }
 };
 
+// Block-value octree (C23): leaf payloads are block ids.  Pre-order emission over the Morton-sorted
+// cells as Builder does; with compaction an octant whose eight children are leaves holding the same
+// block value becomes one leaf of its parent (Octant::is_compactable, new_octree.rs:227-233: all eight
+// leaf bits set and every child value equal -- the reference's rule for leaf children), bottom-up at
+// every level as SectionOctantBuilder::insert_child_and_compact / RegionOctreeBuilder::recursive_build
+// apply it (:688-709, 582-587).  The root stays an octant.
+struct BlockBuilder {
+    octpt_octree *t;
+    const std::vector<std::pair<uint64_t, uint32_t>> &cells;  // (Morton code, block), sorted
+    uint32_t depth;
+    bool compact;
+    struct Child {
+        bool leaf;
+        uint32_t v;
+    };
+    Child node(uint32_t level, size_t lo, size_t hi) {
+        const uint32_t id = (uint32_t)t->octants.size();
+        t->octants.push_back(octpt_octant{0, 0, {0, 0, 0, 0, 0, 0, 0, 0}});
+        const uint32_t shift = 3 * (depth - 1 - level);
+        size_t a = lo;
+        for (uint32_t c = 0; c < 8; ++c) {
+            size_t b = a;
+            while (b < hi && ((cells[b].first >> shift) & 7u) == c) ++b;
+            if (b == a) continue;
+            Child ch{true, cells[a].second};
+            if (level + 1 < depth) ch = node(level + 1, a, b);
+            t->octants[id].child_mask |= (uint16_t)(ch.leaf ? ((1u << c) | (1u << (c + 8))) : (1u << c));
+            t->octants[id].children[c] = ch.v;
+            a = b;
+        }
+        if (compact && level > 0 && t->octants[id].child_mask == 0xFFFFu) {
+            const uint32_t *ch = t->octants[id].children;
+            bool same = true;
+            for (int k = 1; k < 8 && same; ++k) same = ch[k] == ch[0];
+            if (same) {  // eight equal leaves: this octant is the last one emitted
+                const uint32_t v = ch[0];
+                t->octants.pop_back();
+                return Child{true, v};
+            }
+        }
+        return Child{false, id};
+    }
+};
+
 inline int32_t clamp_cell(float f, int32_t hi) {
     if (!(f >= 0.0f)) return 0;  // also NaN
     if (f >= (float)hi) return hi;
@@ -1006,6 +1206,7 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     // OCTPT_DRAIN_RAYS=n: the drain's queue threshold; 0 turns the drain off (A/B)
     const char *drain_env = std::getenv("OCTPT_DRAIN_RAYS");
     if (drain_env && *drain_env) ctx->drain_rays = (uint32_t)std::strtoul(drain_env, nullptr, 10);
+    ctx->mem_limit = (size_t)env_u32("OCTPT_DEVICE_MEM_LIMIT", 0u) << 20;  // MiB, test hook (ensure_wave)
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);
@@ -1018,12 +1219,6 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     if (hipMalloc(&ctx->d_lut_byte, sizeof lb) != hipSuccess) return bail(OCTPT_ERR_OOM);
     if (hipMemcpy(ctx->d_lut_float, lf, sizeof lf, hipMemcpyHostToDevice) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipMemcpy(ctx->d_lut_byte, lb, sizeof lb, hipMemcpyHostToDevice) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
-    if (hipMalloc(&ctx->d_chain, kChainEntries * sizeof(uint4)) != hipSuccess) return bail(OCTPT_ERR_OOM);
-    if (hipMemset(ctx->d_chain, 0, kChainEntries * sizeof(uint4)) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
-    {
-        const char *sc = std::getenv("OCTPT_START_CHAIN");
-        ctx->start_chain = !(sc && sc[0] == '0');
-    }
     *out = ctx;
     return OCTPT_OK;
 }
@@ -1055,7 +1250,6 @@ void octpt_destroy(octpt_ctx *ctx) {
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_lut_float) (void)hipFree(ctx->d_lut_float);
     if (ctx->d_lut_byte) (void)hipFree(ctx->d_lut_byte);
-    if (ctx->d_chain) (void)hipFree(ctx->d_chain);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1078,46 +1272,14 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         // One 8-byte load per descend / leaf visit yields the child's own base and mask.
         std::vector<uint32_t> base(d->octant_count);
         size_t n_slots = 0;
-#if OCTPT_NODE_CACHE
-        // node-cache experiment: the slots of the top OCTPT_NODE_CACHE_LEVELS levels'
-        // octants come first (breadth first), so that extend mirrors [0, n_cached) in LDS
-        std::vector<uint32_t> first;
-        {
-            const uint32_t levels = env_u32("OCTPT_NODE_CACHE_LEVELS", 2u);
-            std::vector<uint32_t> frontier{d->root};
-            std::vector<char> taken(d->octant_count, 0);
-            for (uint32_t l = 0; l < levels && !frontier.empty(); ++l) {
-                size_t add = 0;
-                for (uint32_t o : frontier) add += (size_t)__builtin_popcount(masks[o] & 0xFFu);
-                if (n_slots + add > 1024u) break;  // LDS budget of the cache (8 KB)
-                std::vector<uint32_t> next;
-                for (uint32_t o : frontier) {
-                    if (taken[o]) continue;
-                    taken[o] = 1;
-                    first.push_back(o);
-                    base[o] = (uint32_t)n_slots;
-                    n_slots += (size_t)__builtin_popcount(masks[o] & 0xFFu);
-                    for (int i = 0; i < 8; ++i)
-                        if (((masks[o] >> i) & 1) && !((masks[o] >> (i + 8)) & 1)) next.push_back(d->octants[o].children[i]);
-                }
-                frontier.swap(next);
-            }
-            S.n_cached = (uint32_t)n_slots;
-            for (uint32_t n = 0; n < d->octant_count; ++n) {
-                if (taken[n]) continue;
-                base[n] = (uint32_t)n_slots;
-                n_slots += (size_t)__builtin_popcount(masks[n] & 0xFFu);
-            }
-        }
-#else
         for (uint32_t n = 0; n < d->octant_count; ++n) {
             base[n] = (uint32_t)n_slots;
             n_slots += (size_t)__builtin_popcount(masks[n] & 0xFFu);
         }
-#endif
         if (n_slots >= 0xFFFFFFFFull) return fail(ctx, OCTPT_ERR_INVALID_ARG, "octree too large");
         // + 8 zero slots: a child index computed for an absent child of the last octant stays in bounds
         std::vector<uint2> child(n_slots + 8, make_uint2(0u, 0u));
+        const std::vector<uint32_t> bflags = d->blocks ? block_slot_flags(d) : std::vector<uint32_t>();
         for (uint32_t n = 0; n < d->octant_count; ++n) {
             const octpt_octant &o = d->octants[n];
             uint32_t k = base[n];
@@ -1127,6 +1289,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
                 const uint32_t v = o.children[i];
                 if (!leaf) {
                     child[k++] = make_uint2(base[v], masks[v]);
+                } else if (d->blocks) {  // block-value leaf (C23): (block id, its slot flags)
+                    child[k++] = make_uint2(v, bflags[v]);
                 } else if (d->leaf_count[v] == 1) {  // single-primitive leaf: the prim id itself
                     child[k++] = make_uint2(d->leaf_prims[d->leaf_first[v]], 1u);
                 } else {
@@ -1137,7 +1301,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         // single-sphere leaf slots carry their sphere in a parallel array, so that extend loads it
         // beside the slot instead of after it (sphere-only scenes)
         std::vector<float4> leaf_sph;
-        if (!d->cuboid_count) {
+        if (!d->cuboid_count && !d->blocks) {
             leaf_sph.assign(child.size(), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
             for (uint32_t n = 0; n < d->octant_count; ++n) {
                 const octpt_octant &o = d->octants[n];
@@ -1187,6 +1351,7 @@ octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *d,
     try {
         octpt_status st = validate_head(ctx, d, false);
         if (st != OCTPT_OK) return st;
+        if (d->blocks) return fail(ctx, OCTPT_ERR_INVALID_ARG, "a block-value scene is uploaded with its octree");
         st = validate_tables(ctx, d);
         if (st != OCTPT_OK) return st;
         if (pair_bound(d->spheres, d->sphere_count, d->cuboids, d->cuboid_count, d->depth) > kMaxBuildPairs)
@@ -1501,16 +1666,24 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     ctx->kpending.clear();
     std::vector<unsigned long long> rows(kStatWords);
     HIP_TRY(ctx, hipMemcpy(rows.data(), ctx->d_stats, kStatWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    unsigned long long v[kStatCount] = {0};
+    // rows [0, kSegs): every kernel but the drain; [kStatDrainRow, +kSegs): the drain (octpt_stats::drain)
+    unsigned long long v[kStatCount] = {0}, dr[kStatCount] = {0};
     for (uint32_t r = 0; r < kSegs; ++r)
-        for (uint32_t i = 0; i < kStatCount; ++i) v[i] += rows[r * kStatRow + i];
-    if (std::getenv("OCTPT_PROFILE_LANES")) {  // diagnostic builds (-DOCTPT_PROFILE_LANES) fill words 8..20
+        for (uint32_t i = 0; i < kStatCount; ++i) {
+            v[i] += rows[r * kStatRow + i];
+            dr[i] += rows[(kStatDrainRow + r) * kStatRow + i];
+        }
+    for (uint32_t i = 0; i < kStatCount; ++i) {
+        out->drain[i] = dr[i];
+        v[i] += dr[i];
+    }
+    if (std::getenv("OCTPT_PROFILE_LANES")) {  // diagnostic builds (-DOCTPT_PROFILE_LANES) fill words 12..24
         static const char *names[13] = {"iters", "active", "leaf_it", "leaf_ln", "pop_it", "pop_ln", "push_it",
                                         "desc_ln", "exact", "fold_it", "fold_ln", "dfold_it", "dfold_ln"};
         std::fprintf(stderr, "octpt lanes:");
         for (uint32_t i = 0; i < 13; ++i) {
             unsigned long long x = 0;
-            for (uint32_t r = 0; r < kSegs; ++r) x += rows[r * kStatRow + 8 + i];
+            for (uint32_t r = 0; r < kSegs; ++r) x += rows[r * kStatRow + 12 + i];
             std::fprintf(stderr, " %s=%llu", names[i], x);
         }
         std::fprintf(stderr, "\n");
@@ -1522,6 +1695,11 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     out->cuboid_tests = v[kStatCuboidTests];
     out->shade_events = v[kStatShade];
     out->texel_reads = v[kStatTexels];
+    out->block_tests = v[kStatBlockTests];
+    out->issued_bytes = v[kStatIssued];
+    out->pool_slots = ctx->pool;
+    out->chunk_items = ctx->color_cap;
+    out->wave_allocs = ctx->wave_allocs_n;
     out->launches = ctx->launches;
     out->kernel_ms = ctx->kernel_ms;
     out->extend_launches = ctx->kern_n[0];
@@ -1664,6 +1842,36 @@ octpt_status octpt_build_octree_ex(const octpt_sphere *spheres, uint32_t ns, con
         }
         Builder b{t, std::move(codes), depth, (flags & OCTPT_BUILD_COMPACT) != 0};
         t->root = b.node(0, 0, (uint32_t)b.leaf_code.size()).v;
+        *out = t;
+        return OCTPT_OK;
+    } catch (const std::bad_alloc &) {
+        return OCTPT_ERR_OOM;
+    } catch (...) {
+        return OCTPT_ERR_INTERNAL;
+    }
+}
+
+octpt_status octpt_build_block_octree(const uint32_t *cells, uint32_t n, uint32_t depth, uint32_t flags,
+                                      octpt_octree **out) {
+    if (!out) return OCTPT_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (flags & ~OCTPT_BUILD_COMPACT) return OCTPT_ERR_INVALID_ARG;
+    if (depth < 1 || depth > kMaxDepth || (n && !cells)) return OCTPT_ERR_INVALID_ARG;
+    try {
+        const uint32_t N = 1u << depth;
+        std::vector<std::pair<uint64_t, uint32_t>> sorted(n);
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t *c = cells + 4 * (size_t)k;
+            if (c[0] >= N || c[1] >= N || c[2] >= N || c[3] > kPrimIndexMask) return OCTPT_ERR_INVALID_ARG;
+            sorted[k] = {morton(c[0], c[1], c[2]), c[3]};
+        }
+        std::sort(sorted.begin(), sorted.end());
+        for (size_t k = 1; k < sorted.size(); ++k)
+            if (sorted[k].first == sorted[k - 1].first) return OCTPT_ERR_INVALID_ARG;  // two blocks in one cell
+        octpt_octree *t = new octpt_octree();
+        t->depth = depth;
+        BlockBuilder b{t, sorted, depth, (flags & OCTPT_BUILD_COMPACT) != 0};
+        t->root = b.node(0, 0, sorted.size()).v;
         *out = t;
         return OCTPT_OK;
     } catch (const std::bad_alloc &) {

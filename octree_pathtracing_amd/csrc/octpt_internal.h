@@ -69,8 +69,12 @@ struct alignas(16) DevQuad {
     float4 tv1;    // (texture_v_range.y, 0, 0, 0)
 };
 
-// primitive kinds a kernel instance handles (wf_extend_kernel's kPrims)
-constexpr int kPrimsSpheres = 0, kPrimsBoxes = 1, kPrimsModels = 2;
+// primitive kinds a kernel instance handles (wf_extend_kernel's kPrims); kPrimsBlocks: block-value leaves (C23)
+constexpr int kPrimsSpheres = 0, kPrimsBoxes = 1, kPrimsModels = 2, kPrimsBlocks = 3;
+// flags of a block leaf's slot (slot.y, set at upload): bit f (f < 6) = face f's texture has a texel with
+// alpha 0 (the leaf test reads the texel there), kBlockIsModel = the block is a block model
+constexpr uint32_t kBlockFaceAlphaMask = 0x3Fu;
+constexpr uint32_t kBlockIsModel = 0x40u;
 // self-intersection key of a ray leaving quad q: kQuadKey | q; prim ids are
 // sphere indices < 2^27 or kPrimCuboidBit | index, so the keys never collide
 constexpr uint32_t kQuadKey = 0x40000000u;
@@ -83,7 +87,6 @@ struct DevScene {
     const float4 *leaf_sph;         // parallel to node_child: the sphere of a single-sphere leaf slot
     uint32_t root, root_mask, node0_mask, depth, n_octants;  // root = the root octant's base
     uint32_t has_cuboids;
-    uint32_t n_cached;              // slots [0, n_cached) mirrored in LDS (OCTPT_NODE_CACHE experiment), else 0
     float octree_scale;             // 2^-depth
     float inv_octree_scale;         // 2^depth (x / 2^-depth == x * 2^depth exactly)
     const uint32_t *leaf_prims;
@@ -96,15 +99,17 @@ struct DevScene {
     const uint2 *models;            // (first quad, quad count)
     const DevQuad *quads;
     uint32_t has_models;
+    // block-value leaves (C23): a leaf slot is (block id, kBlock* flags); blk_mat = 6 face materials per
+    // block, blk_model = its model (OCTPT_MODEL_NONE: the block fills its cell)
+    uint32_t has_blocks;
+    const uint32_t *blk_mat;
+    const uint32_t *blk_model;
     const DevMaterial *mats;
     uint32_t n_mats;
     const DevTexture *texs;
     uint32_t n_texs;
     const uint8_t *texels;
     const float *lut_float;         // LUT_TABLE_FLOAT (texture.rs:51-54)
-    // start chain (get_traversal_data's beam start): chain[0].x = n, chain[1 + l] =
-    // (child index, its base, its mask) of the l-th descend of the camera centre ray from the root
-    const uint4 *chain;
     DevSun sun;
     int32_t emitters;
 };
@@ -163,6 +168,7 @@ struct WaveBuffers {
     uint2 *pc;      // (cur_mat, depth | specular << 8 | path_segs << 16)
     uint32_t *item0;  // per slot: the chunk item the seed started there (the first shade rebuilds pa / pb / pc)
     uint2 *hit;     // per queue position: (cuboid bit | flags << 27 | prim index, t) -- hit_record()
+    float2 *huv;    // per queue position, block-value scenes only (C23): the hit's (u, v), or a quad's barycentrics
     float4 *color;  // per chunk item: (L.xyz, path segments)
     // sun-sampling state, 4 planes of `pool` float4:
     // (co.xyz, clast), (cd.xyz, ccur), (cn.xyz, mult), att
@@ -181,11 +187,16 @@ enum StatIndex {
     kStatCuboidTests,
     kStatShade,
     kStatTexels,
+    kStatBlockTests,  // block-value leaf tests (C23)
+    kStatIssued,      // extend's issued load bytes (OCTPT_COUNT_ISSUED builds only)
     kStatCount
 };
-// statistics rows: kSegs rows of kStatRow counters (256 B each), row = blockIdx % kSegs; the host sums
+static_assert(kStatCount == OCTPT_STAT_COUNT, "octpt_stats::drain order");
+// statistics rows: kSegs rows of kStatRow counters (256 B each), row = blockIdx % kSegs; the host sums.
+// The drain kernel counts into a second set of kSegs rows (octpt_stats::drain).
 constexpr uint32_t kStatRow = 32;
-constexpr uint32_t kStatWords = kSegs * kStatRow;
+constexpr uint32_t kStatWords = 2u * kSegs * kStatRow;
+constexpr uint32_t kStatDrainRow = kSegs;
 
 // kernel launchers (octpt_kernels.hip)
 hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
@@ -214,13 +225,6 @@ hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const ui
 hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards,
                           uint32_t stride, float4 *frame, hipStream_t stream);
 int render_blocks_per_cu(uint32_t depth);
-// the start chain of the camera's centre ray (DevScene::chain), one thread.  The replay is compiled
-// out by default: measured -1 % on C3 / C5 and +-0 on preview; -DOCTPT_START_CHAIN=1
-#ifndef OCTPT_START_CHAIN
-#define OCTPT_START_CHAIN 0
-#endif
-constexpr uint32_t kChainEntries = kMaxDepth + 2;
-hipError_t launch_start_chain(const DevScene &S, const DevCamera &C, uint4 *chain, hipStream_t stream);
 size_t render_lds_bytes(uint32_t depth);
 
 // std::vector allocator that leaves resized elements uninitialised: the builders overwrite every

@@ -17,10 +17,6 @@
 // implements as `forward_accumulation`.
 #include "octpt_internal.h"
 
-#ifndef OCTPT_NODE_CACHE
-#define OCTPT_NODE_CACHE 0  // LDS copy of the top octree levels' slots in extend (experiment)
-#endif
-
 namespace octpt {
 namespace {
 
@@ -195,9 +191,6 @@ template <uint32_t kStride>
 struct StackT {
     uint2 *e;
     uint16_t *m;
-#if OCTPT_NODE_CACHE
-    const uint2 *nc;  // LDS copy of node_child[0, S.n_cached): the top octree levels (experiment)
-#endif
 };
 using Stack = StackT<kBlock>;
 
@@ -229,11 +222,22 @@ struct Esvo {
 
 struct Counters {
     uint32_t paths, segs, steps, sph, cub, shade, tex;
+    uint32_t blk;  // block-value leaf tests (C23)
+    uint32_t ib;   // issued load bytes of extend (OCTPT_COUNT_ISSUED builds; see ISSUED below)
 #ifdef OCTPT_PROFILE_LANES  // diagnostic builds: per-wave lane occupancy of extend's step (stat words 8..)
     uint32_t p_iters, p_active, p_leaf_it, p_leaf_ln, p_pop_it, p_pop_ln, p_push_it, p_desc_ln, p_exact, p_fold_it,
         p_fold_ln, p_dfold_it, p_dfold_ln;
 #endif
 };
+
+// Issued-bytes accounting (the honest reading of extend's roofline): a diagnostic build
+// with -DOCTPT_COUNT_ISSUED adds the bytes of every load extend issues -- node slots of the lanes that
+// load one, primitives, quads, alpha texels -- to Counters::ib; the product build compiles it out.
+#ifdef OCTPT_COUNT_ISSUED
+#define ISSUED(cnt, bytes) ((cnt).ib += (uint32_t)(bytes))
+#else
+#define ISSUED(cnt, bytes) ((void)0)
+#endif
 
 #ifdef OCTPT_PROFILE_LANES
 // counted once per wave (by its first active lane): whether any lane has `cond`, and how many
@@ -252,12 +256,9 @@ __device__ __forceinline__ uint32_t f2u32_sat(float f) {
     return (uint32_t)f;
 }
 
-// Texture::value (texture.rs:64-93) for Texture::Image, corrected RGBA stride [C9]; colour
-// textures are pre-converted into the material record at upload
-__device__ inline void texture_image_value(const DevScene &S, uint32_t tex_idx, float u, float v, float out[4],
-                                           Counters &cnt) {
-    const DevTexture t = S.texs[tex_idx];
-    if (t.height == 0u) { out[0] = out[1] = out[2] = out[3] = 1.0f; return; }
+// the RGBA8 texel of Texture::value (texture.rs:64-93) for Texture::Image at (u, v): uv clamped, v
+// flipped, nearest texel, corrected RGBA stride [C9]
+__device__ __forceinline__ uint32_t image_texel(const DevScene &S, const DevTexture &t, float u, float v) {
     float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
     float vv = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
     vv = 1.0f - vv;
@@ -265,7 +266,16 @@ __device__ inline void texture_image_value(const DevScene &S, uint32_t tex_idx, 
     uint32_t j = f2u32_sat(vv * (float)t.height);
     if (i > t.width - 1u) i = t.width - 1u;
     if (j > t.height - 1u) j = t.height - 1u;
-    const uint32_t px = *reinterpret_cast<const uint32_t *>(S.texels + t.offset + ((uint64_t)j * t.width + i) * 4u);
+    return *reinterpret_cast<const uint32_t *>(S.texels + t.offset + ((uint64_t)j * t.width + i) * 4u);
+}
+
+// Texture::value (texture.rs:64-93) for Texture::Image; colour textures are pre-converted into the
+// material record at upload
+__device__ inline void texture_image_value(const DevScene &S, uint32_t tex_idx, float u, float v, float out[4],
+                                           Counters &cnt) {
+    const DevTexture t = S.texs[tex_idx];
+    if (t.height == 0u) { out[0] = out[1] = out[2] = out[3] = 1.0f; return; }
+    const uint32_t px = image_texel(S, t, u, v);
     cnt.tex++;
     out[0] = S.lut_float[px & 255u];
     out[1] = S.lut_float[(px >> 8) & 255u];
@@ -278,6 +288,7 @@ __device__ inline void texture_image_value(const DevScene &S, uint32_t tex_idx, 
 struct PrimHit {
     float t;
     uint32_t f;
+    float u, v;  // block-value leaves (C23): the hit's texture coordinates, or a model quad's barycentrics
     __device__ uint32_t inside() const { return f & 1u; }
     __device__ uint32_t axis() const { return (f >> 1) & 3u; }
     __device__ float nsgn() const { return (f & 8u) ? -1.0f : 1.0f; }
@@ -424,14 +435,16 @@ __device__ __forceinline__ bool cuboid_test(float4 bmin, float4 bmax, const Trac
 // Quad::hit (geometry/quad.rs:172-200) in voxel-local coordinates, with the plane, normal and w
 // derived at upload as Quad::new does (:90-114).  Accepts 0 < t <= t_next (back faces culled).
 __device__ __forceinline__ bool quad_hit(const DevQuad &Q, v3 o_local, v3 d, float t_next, float &t, float &alpha,
-                                         float &beta) {
+                                         float &beta, Counters &cnt) {
     const float4 a = Q.o_d, n4 = Q.n_tv0;
+    ISSUED(cnt, 32);
     const v3 nrm = V(n4.x, n4.y, n4.z);
     const float denom = vdot(d, nrm);
     if (denom >= -RAY_EPSILON) return false;
     t = (a.w - vdot(nrm, o_local)) / denom;
     if (t <= 0.0f || t > t_next) return false;
     const float4 u4 = Q.u_mat, v4 = Q.v_tu0, w4 = Q.w_tu1;
+    ISSUED(cnt, 48);
     const v3 qu = V(u4.x, u4.y, u4.z), qv = V(v4.x, v4.y, v4.z), qw = V(w4.x, w4.y, w4.z);
     const v3 planar = vsub(vadd(o_local, vscale(d, t)), V(a.x, a.y, a.z));
     alpha = vdot(qw, vcross(planar, qv));
@@ -443,8 +456,9 @@ __device__ __forceinline__ bool quad_hit(const DevQuad &Q, v3 o_local, v3 d, flo
 // the closest of the model's quads with 0 < t <= t_accept, ties to the later quad (Quad::hit's
 // `t > t_next` test), skipping the quad the ray leaves (last_prim = kQuadKey | quad)
 __device__ inline bool model_test(const DevScene &S, const TraceRay &r, v3 voxel, uint32_t mdl, float t_accept,
-                                  float &t_best, uint32_t &q_best, float &al_best, float &be_best) {
+                                  float &t_best, uint32_t &q_best, float &al_best, float &be_best, Counters &cnt) {
     const uint2 m = S.models[mdl];
+    ISSUED(cnt, 8);
     const v3 ol = vsub(r.o, voxel);
     float t_next = t_accept;
     bool found = false;
@@ -452,7 +466,7 @@ __device__ inline bool model_test(const DevScene &S, const TraceRay &r, v3 voxel
         const uint32_t q = m.x + k;
         if ((kQuadKey | q) == r.last_prim) continue;
         float t, al, be;
-        if (quad_hit(S.quads[q], ol, r.d, t_next, t, al, be)) {
+        if (quad_hit(S.quads[q], ol, r.d, t_next, t, al, be, cnt)) {
             t_next = t;
             q_best = q;
             al_best = al;
@@ -470,8 +484,157 @@ __device__ __forceinline__ uint32_t face_index(uint32_t axis, float sgn) {
     return sgn > 0.0f ? 4u : 5u;
 }
 
+// A block-value leaf (C23; oracle block_leaf_test): the leaf payload is a block id and the block's box
+// is the leaf cell itself, at any level -- the leaf arm of intersect_octree_path_tracer
+// (octree_traversal.rs:143-214) restated from the ESVO state:
+//  - a block model (slot flag kBlockIsModel, ResourceModel::Quad :207-213): its quads at the cell's
+//    world corner (pos - 1) / octree_scale, closest before the cell exit + tolerance (C1, C19);
+//  - a block filling its cell (ResourceModel::SingleBlock :193-206): passed when t_min == 0 (the ray
+//    starts inside it, :194); else the face is the axis of the cell's largest entry t at pos + scale_exp2
+//    (:156-162), the texture coordinates the entry point's other two coordinates over the cell, flipped
+//    where the ray runs negative (:163-190), |u|, |v| (cuboid.rs:73-90); a face whose texture holds
+//    alpha-0 texels (slot flag bit `face`) reads the texel and lets the ray through where its alpha is
+//    <= EPSILON (SingleBlockModel::intersect, undefined in the reference).  Hit t = t_min / octree_scale.
+// On a hit, prim = face << 27 | block (a full block) or kPrimCuboidBit | quad (a model quad), h.u / h.v =
+// the texture coordinates or the quad's barycentrics.  x / 2^-depth and x / scale_exp2 are the products
+// with the exact power-of-two reciprocals (the oracle divides).
+__device__ inline bool block_leaf_test(const DevScene &S, const TraceRay &r, const Esvo &E, uint2 slot, float tc_max,
+                                       uint32_t &prim, PrimHit &h, Counters &cnt) {
+    cnt.blk++;
+    const float se = E.scale_exp2;
+    const v3 upos = V((E.mirror & 1u) ? (3.0f - se) - E.pos.x : E.pos.x,  // :149-154
+                      (E.mirror & 2u) ? (3.0f - se) - E.pos.y : E.pos.y,
+                      (E.mirror & 4u) ? (3.0f - se) - E.pos.z : E.pos.z);
+    h.f = 0u;
+    if (slot.y & kBlockIsModel) {
+        const float inv = S.inv_octree_scale;
+        const v3 voxel = V((upos.x - 1.0f) * inv, (upos.y - 1.0f) * inv, (upos.z - 1.0f) * inv);
+        const float t_accept = tc_max * inv + CELL_TOL * (se * inv);
+        const uint32_t mdl = S.blk_model[slot.x];
+        ISSUED(cnt, 4);
+        uint32_t q = 0u;
+        float al = 0.0f, be = 0.0f;
+        if (!model_test(S, r, voxel, mdl, t_accept, h.t, q, al, be, cnt)) return false;
+        prim = kPrimCuboidBit | q;
+        h.u = al;
+        h.v = be;
+        return true;
+    }
+    if (E.t_min == 0.0f) return false;
+    const float inv_se = __uint_as_float(0x7F000000u - __float_as_uint(se));  // 1 / scale_exp2, exact
+    const v3 tcn = vsub(vmul(vadd(E.pos, V(se, se, se)), E.t_coef), E.t_bias);  // :156
+    const float tc_min = tmax3(tcn);
+    // ro and the clamped rd of esvo_begin (:71-93)
+    const v3 ro = vadd(vscale(r.o, S.octree_scale), V(1.0f, 1.0f, 1.0f));
+    v3 rd = r.d;
+    const uint32_t epsb = __float_as_uint(OCTREE_EPSILON) & 0x7FFFFFFFu;
+    if (fabsf(rd.x) < OCTREE_EPSILON) rd.x = __uint_as_float(epsb | (__float_as_uint(rd.x) & 0x80000000u));
+    if (fabsf(rd.y) < OCTREE_EPSILON) rd.y = __uint_as_float(epsb | (__float_as_uint(rd.y) & 0x80000000u));
+    if (fabsf(rd.z) < OCTREE_EPSILON) rd.z = __uint_as_float(epsb | (__float_as_uint(rd.z) & 0x80000000u));
+    uint32_t axis;
+    float u, v;
+    bool neg;
+    if (tcn.x == tc_min) {  // :163-171
+        axis = 0u;
+        u = ((ro.z + rd.z * tcn.x) - upos.z) * inv_se;
+        v = ((ro.y + rd.y * tcn.x) - upos.y) * inv_se;
+        neg = rd.x < 0.0f;
+        if (neg) u = 1.0f - u;
+    } else if (tcn.y == tc_min) {  // :172-180
+        axis = 1u;
+        u = ((ro.x + rd.x * tcn.y) - upos.x) * inv_se;
+        v = ((ro.z + rd.z * tcn.y) - upos.z) * inv_se;
+        neg = rd.y < 0.0f;
+        if (neg) v = 1.0f - v;
+    } else {  // :181-189
+        axis = 2u;
+        u = ((ro.x + rd.x * tcn.z) - upos.x) * inv_se;
+        v = ((ro.y + rd.y * tcn.z) - upos.y) * inv_se;
+        neg = rd.z < 0.0f;
+        if (neg) u = 1.0f - u;
+    }
+    u = fabsf(u);
+    v = fabsf(v);
+    const uint32_t face = face_index(axis, neg ? 1.0f : -1.0f);  // the face entered faces against the ray
+    if ((slot.y >> face) & 1u) {  // a face with alpha-0 texels: SingleBlockModel::intersect's texel
+        const uint32_t mat = S.blk_mat[6u * slot.x + face];
+        const DevMaterial &m = S.mats[mat];
+        ISSUED(cnt, 8);
+        float alpha;
+        if (m.texture_kind == 0u) {
+            alpha = m.color[3];
+        } else {
+            const DevTexture t = S.texs[m.texture_index];
+            ISSUED(cnt, 32 + 4);
+            alpha = t.height == 0u ? 1.0f : (float)(image_texel(S, t, u, v) >> 24) / 255.0f;
+        }
+        if (!(alpha > RAY_EPSILON)) return false;
+    }
+    prim = (face << 27) | slot.x;
+    h.t = E.t_min * S.inv_octree_scale;
+    h.u = u;
+    h.v = v;
+    return true;
+}
+
+// the material's colour at (u, v) into r.col (Texture::value, colour textures pre-converted)
+__device__ __forceinline__ void material_color(const DevScene &S, uint32_t mat, float u, float v, PathState &r,
+                                               Counters &cnt) {
+    const DevMaterial &m = S.mats[mat];
+    if (m.texture_kind == 0u) {
+        r.col[0] = m.color[0];
+        r.col[1] = m.color[1];
+        r.col[2] = m.color[2];
+        r.col[3] = m.color[3];
+    } else {
+        texture_image_value(S, m.texture_index, u, v, r.col, cnt);
+    }
+}
+
+// Commit of a block-value leaf hit (C23, oracle commit_hit's block branches) [C1]: x = face << 27 | block
+// (a block filling its cell: the face's normal and material, (hu, hv) its texture coordinates, no
+// self-intersection key -- a ray starting in the block's cell passes it) or kPrimCuboidBit | quad (a
+// block model's quad: its normal and material, uv from the barycentrics (hu, hv) as quad.rs:194-197, the
+// quad's key kQuadKey | q, C19).
+__device__ inline void commit_block_hit(const DevScene &S, PathState &r, uint32_t x, float t, float hu, float hv,
+                                        Counters &cnt) {
+    const v3 p = vadd(r.o, vscale(r.d, t));
+    uint32_t mat, key;
+    float u, v;
+    v3 n;
+    if (x & kPrimCuboidBit) {
+        const uint32_t q = x & kPrimIndexMask;
+        const DevQuad &Q = S.quads[q];
+        n = V(Q.n_tv0.x, Q.n_tv0.y, Q.n_tv0.z);
+        mat = __float_as_uint(Q.u_mat.w);
+        const float tu0 = Q.v_tu0.w, tu1 = Q.w_tu1.w, tv0 = Q.n_tv0.w, tv1 = Q.tv1.x;
+        u = tu0 + hu * (tu1 - tu0);
+        v = tv0 + hv * (tv1 - tv0);
+        key = kQuadKey | q;
+    } else {
+        const uint32_t face = x >> 27, block = x & kPrimIndexMask;
+        mat = S.blk_mat[6u * block + face];
+        // Face::to_normal (cuboid.rs:20-29): W -X, E +X, Bottom -Y, Top +Y, South +Z, North -Z
+        const float sgn = (face == 1u || face == 3u || face == 4u) ? 1.0f : -1.0f;
+        n = V(0.0f, 0.0f, 0.0f);
+        if (face < 2u) n.x = sgn; else if (face < 4u) n.y = sgn; else n.z = sgn;
+        u = hu;
+        v = hv;
+        key = kPrimNone;
+    }
+    r.o = p;
+    r.n = n;
+    r.last_prim = key;
+    r.cur = mat;
+    material_color(S, mat, u, v, r, cnt);
+}
+
 // Chunky-style commit [C1]: the ray origin moves to the hit point
 __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim, const PrimHit &h, Counters &cnt) {
+    if (S.has_blocks) {
+        commit_block_hit(S, r, prim, h.t, h.u, h.v, cnt);
+        return;
+    }
     const v3 p = vadd(r.o, vscale(r.d, h.t));
     float u = 0.0f, v = 0.0f;
     uint32_t mat;
@@ -501,7 +664,7 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
             tr.d = r.d;
             tr.last_prim = r.last_prim;
             tr.self_inward = false;
-            model_test(S, tr, V(ca.x, ca.y, ca.z), mdl, h.t, tq, q, al, be);
+            model_test(S, tr, V(ca.x, ca.y, ca.z), mdl, h.t, tq, q, al, be, cnt);
             const DevQuad &Q = S.quads[q];
             n = V(Q.n_tv0.x, Q.n_tv0.y, Q.n_tv0.z);
             mat = __float_as_uint(Q.u_mat.w);
@@ -568,9 +731,6 @@ __device__ __forceinline__ void stk_write(const StackT<kS> &stk, uint32_t slot, 
 template <uint32_t kS = kBlock>
 __device__ __forceinline__ StackT<kS> stack_of(uint2 *lds, uint32_t depth) {
     StackT<kS> s;
-#if OCTPT_NODE_CACHE
-    s.nc = nullptr;  // only wf_extend_kernel loads the cache; the other kernels get n_cached = 0
-#endif
     s.e = lds + threadIdx.x;
     s.m = reinterpret_cast<uint16_t *>(lds + (size_t)(depth - 1u) * kS) + threadIdx.x;
     return s;
@@ -618,6 +778,9 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (upper.y > E.t_min) { E.idx ^= 2u; E.pos.y = 1.5f; }
     if (upper.z > E.t_min) { E.idx ^= 4u; E.pos.z = 1.5f; }
     E.iter = 0u;
+#ifdef OCTPT_ZERO_STACK  // diagnostic: the oracle's zeroed stack (octant 0, t 0) instead of stale entries
+    for (uint32_t l = 0; l + 1u < S.depth; ++l) stk_write(stk, l, 0u, 0.0f, S.node0_mask);
+#endif
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
@@ -646,49 +809,6 @@ __device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uin
 }
 
 
-// Start chain (get_traversal_data's beam start, octree_traversal.rs:537-714, meant for
-// CameraUniform.traversal_start_idx, gpu_renderer.rs:579-581).  S.chain holds the descends the
-// camera's centre ray makes from the root.  A ray whose first iterations are descends into the same
-// children runs them here as exact replicas of esvo_step's descend (same stop tests, t-values, push
-// and child choice, counted in E.iter) with the child slots taken from the chain (scalar loads)
-// instead of node_child: coherent primary rays skip the top levels' loads and step overhead.  A lane
-// leaves the replay at the first level where its iteration would not descend into the chain's child.
-template <uint32_t kS>
-__device__ __forceinline__ void esvo_start_chain(const DevScene &S, Esvo &E, const StackT<kS> &stk,
-                                                 const uint4 *__restrict__ chain) {
-#if OCTPT_START_CHAIN
-    const float max_dst = MAX_DST_WORLD * S.octree_scale;
-    const uint32_t n = chain[0].x;  // wave-uniform (LDS)
-    uint4 c = chain[1];
-    for (uint32_t l = 0; l < n; ++l) {
-        const uint4 cn = chain[2u + l];  // the next entry's LDS read overlaps this level (kChainEntries + 1 slots)
-        const v3 tc = vsub(vmul(E.pos, E.t_coef), E.t_bias);
-        const float tc_max = tmin3(tc);
-        const float tv_max = tmn(E.t_max, tc_max);
-        // esvo_step's descend test: the chain's child is an octant of the same parent
-        const bool d = ((E.idx ^ E.mirror) == c.x) & (E.iter < OCTREE_MAX_STEPS) & !(E.t_min > max_dst) &
-                       (E.t_min <= tv_max);
-        if (!d) break;
-        esvo_descend(E, stk, S.depth, tc, tc_max, tv_max, make_uint2(c.y, c.z));
-        c = cn;
-    }
-#endif
-}
-
-// LDS copy of the start chain (kChainEntries + 1 uint4 after the block's stack rows), block-wide
-constexpr uint32_t kChainLdsBytes = OCTPT_START_CHAIN ? (kChainEntries + 1u) * 16u : 0u;
-__device__ __forceinline__ const uint4 *chain_to_lds(const DevScene &S, uint2 *lds) {
-#if OCTPT_START_CHAIN
-    uint4 *c = reinterpret_cast<uint4 *>(lds + (size_t)(S.depth - 1u) * kBlock * 10u / 8u);
-    if (threadIdx.x < kChainEntries) c[threadIdx.x] = S.chain[threadIdx.x];
-    if (threadIdx.x == kChainEntries) c[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-    return c;
-#else
-    return nullptr;
-#endif
-}
-
 #ifndef OCTPT_FOLD
 #define OCTPT_FOLD 1  // absent-sibling folds per step (A/B: -DOCTPT_FOLD=0)
 #endif
@@ -716,21 +836,25 @@ __device__ __forceinline__ bool prim_test(const DevScene &S, const TraceRay &r, 
     bool ok;
     if (kPrims == kPrimsSpheres || !(prim & kPrimCuboidBit)) {
         cnt.sph++;
+        ISSUED(cnt, 16);
         ok = sphere_test(S.spheres[prim], r, self_prim, h);
     } else {
         cnt.cub++;
         const uint32_t ci = prim & ~kPrimCuboidBit;
         const float4 ca = S.cub_a[ci];
+        ISSUED(cnt, 16);
         if (kPrims == kPrimsModels && S.has_models) {
             const uint32_t mdl = S.cub_model[ci];
+            ISSUED(cnt, 4);
             if (mdl != OCTPT_MODEL_NONE) {
                 uint32_t q;
                 float al, be;
                 h.f = 0u;
-                return model_test(S, r, V(ca.x, ca.y, ca.z), mdl, t_accept, h.t, q, al, be);
+                return model_test(S, r, V(ca.x, ca.y, ca.z), mdl, t_accept, h.t, q, al, be, cnt);
             }
         }
         const float2 cb = S.cub_b[ci];
+        ISSUED(cnt, 8);
         // 1/d without the three correctly-rounded divides: ESVO's t_coef holds the same quotients
         const v3 inv = inv_dir_of(r.d, E.t_coef, E.mirror);
         ok = cuboid_test(make_float4(ca.x, ca.y, ca.z, 0.0f), make_float4(ca.w, cb.x, cb.y, 0.0f), r, inv, self_prim, h);
@@ -748,10 +872,14 @@ template <int kPrims = kPrimsModels, bool kFast = false>
 __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, const Esvo &E, uint2 lr, float t_accept,
                                  uint32_t &best_prim, PrimHit &best, Counters &cnt, const float4 *pre = nullptr) {
     uint32_t prim = lr.x;
-    if (lr.y != 1u) prim = S.leaf_prims[lr.x];
+    if (lr.y != 1u) {
+        prim = S.leaf_prims[lr.x];
+        ISSUED(cnt, 4);
+    }
     bool found;
     if (kFast && lr.y == 1u && (kPrims == kPrimsSpheres || !(prim & kPrimCuboidBit))) {
         cnt.sph++;
+        if (!(kPrims == kPrimsSpheres && pre)) ISSUED(cnt, 16);
         const float4 sp = (kPrims == kPrimsSpheres && pre) ? *pre : S.spheres[prim];
         const bool self_prim = prim == r.last_prim;
         const int d = sphere_decide(sp, r, self_prim, t_accept, best);
@@ -773,6 +901,7 @@ __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, const Esv
     if (found) best_prim = prim;
     for (uint32_t k = 1; k < lr.y; ++k) {
         const uint32_t p = S.leaf_prims[lr.x + k];
+        ISSUED(cnt, 4);
         PrimHit hk;
         if (prim_test<kPrims>(S, r, E, p, t_accept, hk, cnt) && (!found || hk.t < best.t)) {
             best = hk;
@@ -807,14 +936,16 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const bool descend = (kind == 0x001u) & !stopped & (E.t_min <= tv_max);
     uint2 slot = make_uint2(0u, 0u);
     const uint32_t sidx = E.parent + __popc(E.pmask & ((1u << cidx) - 1u));
-#if OCTPT_NODE_CACHE
-    if (take_leaf || descend) slot = sidx < S.n_cached ? stk.nc[sidx] : S.node_child[sidx];
-#else
-    if (take_leaf || descend) slot = S.node_child[sidx];
-#endif
+    if (take_leaf || descend) {
+        slot = S.node_child[sidx];
+        ISSUED(cnt, 8);
+    }
     // sphere-only scenes: a leaf's first sphere is loaded beside its slot (no dependent second load)
     float4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (kPrims == kPrimsSpheres && take_leaf) lsph = S.leaf_sph[sidx];
+    if (kPrims == kPrimsSpheres && take_leaf) {
+        lsph = S.leaf_sph[sidx];
+        ISSUED(cnt, 16);
+    }
 #ifdef OCTPT_PROFILE_LANES
     prof_wave(cnt.p_leaf_it, cnt.p_leaf_ln, take_leaf);
     prof_wave(cnt.p_push_it, cnt.p_desc_ln, descend);
@@ -826,8 +957,11 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const float t_accept = tc_max * S.inv_octree_scale + CELL_TOL * cell_w;
         // a hit lane runs the advance below too (its state is discarded): the descend / advance
         // block then needs no exec-mask region of its own
-        leaf_hit = leaf_test<kPrims, kFast>(S, ray, E, slot, t_accept, prim, h, cnt,
-                                            kPrims == kPrimsSpheres ? &lsph : nullptr);
+        if constexpr (kPrims == kPrimsBlocks)
+            leaf_hit = block_leaf_test(S, ray, E, slot, tc_max, prim, h, cnt);
+        else
+            leaf_hit = leaf_test<kPrims, kFast>(S, ray, E, slot, t_accept, prim, h, cnt,
+                                                kPrims == kPrimsSpheres ? &lsph : nullptr);
     }
     // Descend (:216-244) and advance (:249-260) as one select-based update: every lane computes
     // X = t_coef * f + t_corner with f = half for descend (X = t_center) and f = 0 otherwise
@@ -878,6 +1012,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
 #endif
         if (d2) {
             const uint2 slot2 = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx2) - 1u))];
+            ISSUED(cnt, 8);
             esvo_descend(E, stk, S.depth, tc2, tc2_max, tv2_max, slot2);
         }
     }
@@ -1329,24 +1464,27 @@ __device__ inline unsigned long long wave_sum(uint32_t v) {
     return s;
 }
 
-__device__ inline void flush_counters(const Counters &cnt, unsigned long long *stats) {
+// row_base: 0, or kStatDrainRow for the drain kernel (its share is reported apart, octpt_stats::drain)
+__device__ inline void flush_counters(const Counters &cnt, unsigned long long *stats, uint32_t row_base = 0u) {
 #ifdef OCTPT_NO_STATS  // A/B builds only: every counter update becomes dead code
     return;
 #endif
 #ifdef OCTPT_PROFILE_LANES
-    constexpr int kN = kStatCount + 1 + 13;
-    const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex, 0u,
+    constexpr int kN = 12 + 13;  // profile words from 12 on (octpt_get_stats prints them)
+    const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex, cnt.blk, cnt.ib,
+                               0u, 0u, 0u,
                                cnt.p_iters, cnt.p_active, cnt.p_leaf_it, cnt.p_leaf_ln, cnt.p_pop_it, cnt.p_pop_ln,
                                cnt.p_push_it, cnt.p_desc_ln, cnt.p_exact, cnt.p_fold_it, cnt.p_fold_ln,
                                cnt.p_dfold_it, cnt.p_dfold_ln};
 #else
     constexpr int kN = kStatCount;
-    const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex};
+    const uint32_t vals[kN] = {cnt.paths, cnt.segs, cnt.steps, cnt.sph, cnt.cub, cnt.shade, cnt.tex, cnt.blk, cnt.ib};
 #endif
 #pragma unroll
     for (int i = 0; i < kN; ++i) {
         const unsigned long long s = wave_sum(vals[i]);
-        if ((threadIdx.x & 63u) == 0u && s) atomicAdd(&stats[(blockIdx.x % kSegs) * kStatRow + i], s);
+        if ((threadIdx.x & 63u) == 0u && s)
+            atomicAdd(&stats[(row_base + blockIdx.x % kSegs) * kStatRow + i], s);
     }
 }
 
@@ -1366,7 +1504,7 @@ __device__ __forceinline__ uint32_t wave_ticket(uint32_t *ctr, bool want) {
 // ===========================================================================
 enum : uint32_t { ST_IDLE = 0, ST_NEWPATH, ST_BEGIN, ST_TRAV, ST_HIT, ST_MISS, ST_FINISH, ST_DONE };
 
-template <bool kNee>
+template <bool kNee, int kPrims>
 __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C, DevRender R, float4 *__restrict__ accum,
                                                         uint32_t *__restrict__ segcount, uint32_t *__restrict__ counter,
                                                         unsigned long long *__restrict__ stats) {
@@ -1430,7 +1568,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             }
             first = false;
             if (state == ST_TRAV) {
-                const int rs = esvo_step(S, tr, E, stk, cnt, hprim, hh);
+                const int rs = esvo_step<kPrims>(S, tr, E, stk, cnt, hprim, hh);
                 if (rs == kStepHit) state = ST_HIT;
                 else if (rs == kStepMiss) state = ST_MISS;
                 if (rs != kStepContinue) cnt.steps += E.iter;
@@ -1457,6 +1595,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             }
         }
     }
+    cnt.ib = 0u;  // issued bytes are extend's only
     flush_counters(cnt, stats);
 }
 
@@ -1472,14 +1611,13 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
 #endif
 // one wave per SIMD above the natural allocation (78 / 86 / 102 VGPRs -> 72 / 80 / 96), as for extend
 #define OCTPT_PREVIEW_WAVES_OF(k) \
-    (OCTPT_PREVIEW_BOUNDS ? ((k) == kPrimsSpheres ? 7 : (k) == kPrimsBoxes ? 6 : 5) : 1)
+    (OCTPT_PREVIEW_BOUNDS ? ((k) == kPrimsSpheres ? 7 : ((k) == kPrimsBoxes || (k) == kPrimsBlocks) ? 6 : 5) : 1)
 template <int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void preview_kernel(DevScene S, DevCamera C, DevRender R,
                                                          float4 *__restrict__ accum, uint32_t *__restrict__ segcount,
                                                          unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
     const Stack stk = stack_of(lds_stack, S.depth);
-    const uint4 *chain = chain_to_lds(S, lds_stack);
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     const uint32_t item = blockIdx.x * kBlock + threadIdx.x;
     uint32_t x = 0u, y = 0u;
@@ -1512,7 +1650,6 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
             const TraceRay tr = trace_ray_of(S, ps);
             Esvo E;
             esvo_begin(S, tr, E, stk);
-            esvo_start_chain(S, E, stk, chain);
             uint32_t prim = kPrimNone;
             PrimHit h;
             int rs;
@@ -1540,36 +1677,8 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
         accum[ai] = fb;
         if (segcount) segcount[ai] += pix_segs;
     }
+    cnt.ib = 0u;  // issued bytes are extend's only
     flush_counters(cnt, stats);
-}
-
-// The start chain (DevScene::chain) of the camera's centre ray, Camera::get_ray(0, 0) (camera.rs:77-86,
-// the ray gpu_renderer.rs:579-581 hands get_traversal_data): ESVO from the root while its
-// iteration is a descend into an octant child, recording each child index and slot.  One thread.
-__global__ void start_chain_kernel(DevScene S, DevCamera C, uint4 *__restrict__ chain) {
-    if (threadIdx.x != 0u || blockIdx.x != 0u) return;
-    uint2 e_store[kMaxDepth];
-    uint16_t m_store[kMaxDepth];
-    StackT<1> stk{e_store, m_store};  // pushes of the walk go to a private stack
-    const v3 d = vnorm(vscale(V(C.dir[0], C.dir[1], C.dir[2]), C.d_factor));
-    const TraceRay tr = make_trace_ray(S, V(C.eye[0], C.eye[1], C.eye[2]), d, kPrimNone, false);
-    Esvo E;
-    esvo_begin(S, tr, E, stk);
-    const float max_dst = MAX_DST_WORLD * S.octree_scale;
-    uint32_t n = 0u;
-    for (; n + 1u < S.depth; ++n) {  // a chain ends above the leaf cells
-        const v3 tc = vsub(vmul(E.pos, E.t_coef), E.t_bias);
-        const float tc_max = tmin3(tc);
-        const float tv_max = tmn(E.t_max, tc_max);
-        const uint32_t cidx = E.idx ^ E.mirror;
-        const bool d2 = (((E.pmask >> cidx) & 0x101u) == 0x001u) & (E.iter < OCTREE_MAX_STEPS) &
-                        !(E.t_min > max_dst) & (E.t_min <= tv_max);
-        if (!d2) break;
-        const uint2 slot = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx) - 1u))];
-        chain[1u + n] = make_uint4(cidx, slot.x, slot.y, 0u);
-        esvo_descend(E, stk, S.depth, tc, tc_max, tv_max, slot);
-    }
-    chain[0] = make_uint4(n, 0u, 0u, 0u);
 }
 
 // ===========================================================================
@@ -1779,8 +1888,12 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #ifndef OCTPT_MDL_WAVES
 #define OCTPT_MDL_WAVES 6  // 95 -> 80 VGPRs, 36 B/lane spilled: C5 +5.4 %
 #endif
-#define OCTPT_EXTEND_WAVES_OF(k) \
-    ((k) == kPrimsSpheres ? OCTPT_SPH_WAVES : (k) == kPrimsBoxes ? OCTPT_BOX_WAVES : OCTPT_MDL_WAVES)
+#ifndef OCTPT_BLK_WAVES
+#define OCTPT_BLK_WAVES 7  // block-value leaves (C23)
+#endif
+#define OCTPT_EXTEND_WAVES_OF(k)                                                                              \
+    ((k) == kPrimsSpheres ? OCTPT_SPH_WAVES                                                                   \
+                          : (k) == kPrimsBoxes ? OCTPT_BOX_WAVES : (k) == kPrimsBlocks ? OCTPT_BLK_WAVES : OCTPT_MDL_WAVES)
 // positions a wave claims from its segment at a time (one atomic per claim)
 #ifndef OCTPT_CLAIM
 #define OCTPT_CLAIM 64
@@ -1801,17 +1914,7 @@ template <int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            unsigned long long *__restrict__ stats) {
     extern __shared__ uint2 lds_stack[];
-#if OCTPT_NODE_CACHE
-    Stack stk = stack_of(lds_stack, S.depth);
-    {  // the top levels' slots (the upload puts them first, DESIGN.md §8 node-cache experiment)
-        uint2 *nc = lds_stack + (size_t)(S.depth - 1u) * kBlock * 10u / 8u + kChainLdsBytes / 8u;
-        for (uint32_t i = threadIdx.x; i < S.n_cached; i += kBlock) nc[i] = S.node_child[i];
-        stk.nc = nc;
-    }
-#else
     const Stack stk = stack_of(lds_stack, S.depth);
-#endif
-    const uint4 *chain = chain_to_lds(S, lds_stack);
     const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
     if (blockIdx.x == 0 && threadIdx.x < kSegs) {  // the other queue is refilled by this iteration's shade
         B.ctrl[ctr_count(q ^ 1u, threadIdx.x)] = 0u;
@@ -1869,7 +1972,6 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                     tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk);
-                    esvo_start_chain(S, E, stk, chain);
                     active = true;
                     lane_rays++;
                 }
@@ -1896,7 +1998,12 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 PrimHit h;
                 const int rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
                 if (rs != kStepContinue) {
-                    B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                    if constexpr (kPrims == kPrimsBlocks) {  // (face << 27 | block or the quad, t) + (u, v) (C23)
+                        B.hit[pos] = rs == kStepHit ? make_uint2(prim, __float_as_uint(h.t)) : make_uint2(kPrimNone, 0u);
+                        if (rs == kStepHit) B.huv[pos] = make_float2(h.u, h.v);
+                    } else {
+                        B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                    }
                     cnt.steps += E.iter;
                     active = false;
                 }
@@ -1917,7 +2024,8 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
 template <bool kNee>
 __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C, const DevRender &R,
                                            const WaveBuffers &B, bool first, float4 r0, float4 r1, const uint2 *hit_rec,
-                                           PathState &ps, uint32_t &slot, uint32_t &item, Counters &cnt) {
+                                           const float2 *huv_rec, PathState &ps, uint32_t &slot, uint32_t &item,
+                                           Counters &cnt) {
     slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
     if (first) {
         item = B.item0[slot];
@@ -1934,7 +2042,11 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     if (was_shadow) load_nee(B, slot, ps);
     const uint2 hr = *hit_rec;
     const bool hit = hr.x != kPrimNone;
-    if (hit) {
+    if (hit && S.has_blocks) {  // block-value leaf (C23): the record's (u, v) beside it
+        const float2 uv = *huv_rec;
+        ps.n = V(0.0f, 0.0f, 0.0f);
+        commit_block_hit(S, ps, hr.x, __uint_as_float(hr.y), uv.x, uv.y, cnt);
+    } else if (hit) {
         PrimHit h;
         const uint32_t flags = (hr.x >> 27) & 15u;
         h.t = __uint_as_float(hr.y);
@@ -2009,7 +2121,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
         PathState ps;
         if (valid) {
             const float4 r0 = B.ray0[q][i], r1 = B.ray1[q][i];
-            append = shade_lane<kNee>(S, C, R, B, first != 0u, r0, r1, B.hit + i, ps, slot, item, cnt);
+            append = shade_lane<kNee>(S, C, R, B, first != 0u, r0, r1, B.hit + i, B.huv + i, ps, slot, item, cnt);
             finished = !append;
         }
         // regenerate: finished lanes take the next chunk items (path regeneration)
@@ -2017,6 +2129,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
         const uint32_t t = wave_ticket(B.ctrl + ctr_count(q ^ 1u, seg), append);
         if (append) store_ray(B, q ^ 1u, seg0 + t, slot, ps);
     }
+    cnt.ib = 0u;  // issued bytes are extend's only
     flush_counters(cnt, stats);
 }
 
@@ -2054,10 +2167,15 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                 } while (rs == kStepContinue);
                 cnt.steps += E.iter;
                 cnt.segs++;
-                const uint2 hr = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                uint2 hr;
+                if constexpr (kPrims == kPrimsBlocks)
+                    hr = rs == kStepHit ? make_uint2(prim, __float_as_uint(h.t)) : make_uint2(kPrimNone, 0u);
+                else
+                    hr = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                const float2 huv = make_float2(h.u, h.v);
                 PathState ps;
                 uint32_t slot, item;
-                if (!shade_lane<kNee>(S, DevCamera{}, R, B, false, r0, r1, &hr, ps, slot, item, cnt)) break;
+                if (!shade_lane<kNee>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item, cnt)) break;
                 // the next segment's ray record, as store_ray writes it
                 r0 = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.last_prim));
                 r1 = make_float4(ps.d.x, ps.d.y, ps.d.z,
@@ -2065,7 +2183,7 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
             }
         }
     }
-    flush_counters(cnt, stats);
+    flush_counters(cnt, stats, kStatDrainRow);
 }
 
 // resolve: per pixel, the chunk's samples in sample order into the running mean
@@ -2110,6 +2228,7 @@ __global__ __launch_bounds__(kBlock) void wf_resolve_kernel(DevRender R, WaveBuf
 }
 
 // one ray per thread closest-hit query (Scene::hit) for octpt_intersect
+template <int kPrims>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const float *__restrict__ rays,
                                                            const uint32_t *__restrict__ last_prim,
                                                            const float *__restrict__ last_normal, uint32_t n,
@@ -2134,12 +2253,14 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
     PrimHit h;
     int rs;
     do {
-        rs = esvo_step(S, tr, E, stk, cnt, prim, h);
+        rs = esvo_step<kPrims>(S, tr, E, stk, cnt, prim, h);
     } while (rs == kStepContinue);
     if (rs == kStepHit) {
         commit_hit(S, ps, prim, h, cnt);
         out_t[i] = h.t;
-        out_prim[i] = prim;
+        // block-value scenes (C23): the block id of a block filling its cell, kQuadKey | quad of a model quad
+        out_prim[i] = kPrims != kPrimsBlocks ? prim : ((prim & kPrimCuboidBit) ? kQuadKey | (prim & kPrimIndexMask)
+                                                                                 : prim & kPrimIndexMask);
         if (out_normal) {
             out_normal[3 * i] = ps.n.x;
             out_normal[3 * i + 1] = ps.n.y;
@@ -2181,7 +2302,7 @@ size_t render_lds_bytes(uint32_t depth) { return (size_t)(depth - 1u) * kBlock *
 
 int render_blocks_per_cu(uint32_t depth) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void *>(render_kernel<true>),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void *>(render_kernel<true, kPrimsModels>),
                                                      kBlock, render_lds_bytes(depth)) != hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
@@ -2189,24 +2310,15 @@ int render_blocks_per_cu(uint32_t depth) {
 
 // the extend instance a scene launches: the primitive kinds it holds (sphere-only scenes: no slab test)
 static const void *extend_instance(const DevScene &S) {
+    if (S.has_blocks) return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsBlocks>);
     if (S.has_models) return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsModels>);
     if (S.has_cuboids) return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsBoxes>);
     return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsSpheres>);
 }
 
-// stack rows + the start chain (+ the node-cache experiment's slots)
-static size_t extend_lds_bytes(const DevScene &S) {
-    const size_t b = render_lds_bytes(S.depth) + kChainLdsBytes;
-#if OCTPT_NODE_CACHE
-    return b + (size_t)S.n_cached * sizeof(uint2);
-#else
-    return b;
-#endif
-}
-
 int extend_blocks_per_cu(const DevScene &S) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S), kBlock, extend_lds_bytes(S)) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S), kBlock, render_lds_bytes(S.depth)) !=
         hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
@@ -2214,36 +2326,29 @@ int extend_blocks_per_cu(const DevScene &S) {
 
 hipError_t launch_preview(const DevScene &S0, const DevCamera &C, const DevRender &R, float4 *accum,
                           uint32_t *segcount, unsigned long long *stats, hipStream_t stream) {
-    DevScene S = S0;
-    S.n_cached = 0;  // only wf_extend_kernel mirrors the top slots in LDS
+    const DevScene &S = S0;
     const uint32_t grid = (R.total_items + kBlock - 1u) / kBlock;
     // the primitive kinds of the scene pick the instance, as for wf_extend_kernel
-    const void *fn = S.has_models ? reinterpret_cast<const void *>(preview_kernel<kPrimsModels>)
+    const void *fn = S.has_blocks   ? reinterpret_cast<const void *>(preview_kernel<kPrimsBlocks>)
+                     : S.has_models ? reinterpret_cast<const void *>(preview_kernel<kPrimsModels>)
                      : S.has_cuboids ? reinterpret_cast<const void *>(preview_kernel<kPrimsBoxes>)
                                      : reinterpret_cast<const void *>(preview_kernel<kPrimsSpheres>);
     void *args[] = {const_cast<DevScene *>(&S), const_cast<DevCamera *>(&C), const_cast<DevRender *>(&R), &accum,
                     &segcount, &stats};
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args,
-                                         render_lds_bytes(S.depth) + kChainLdsBytes, stream);
+                                         render_lds_bytes(S.depth), stream);
     if (e != hipSuccess) return e;
-    return hipGetLastError();
-}
-
-hipError_t launch_start_chain(const DevScene &S, const DevCamera &C, uint4 *chain, hipStream_t stream) {
-    hipLaunchKernelGGL(start_chain_kernel, dim3(1), dim3(64), 0, stream, S, C, chain);
     return hipGetLastError();
 }
 
 hipError_t launch_render(const DevScene &S0, const DevCamera &C, const DevRender &R, float4 *accum, uint32_t *segcount,
                          uint32_t *counter, unsigned long long *stats, int grid, hipStream_t stream) {
-    DevScene S = S0;
-    S.n_cached = 0;  // only wf_extend_kernel mirrors the top slots in LDS
-    if (S.sun.sun_sampling)
-        hipLaunchKernelGGL(render_kernel<true>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R,
-                           accum, segcount, counter, stats);
-    else
-        hipLaunchKernelGGL(render_kernel<false>, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R,
-                           accum, segcount, counter, stats);
+    const DevScene &S = S0;
+    // the general instance (spheres, cuboids, cuboid models) or the block-value one (C23)
+    auto kern = S.sun.sun_sampling ? (S.has_blocks ? render_kernel<true, kPrimsBlocks> : render_kernel<true, kPrimsModels>)
+                                   : (S.has_blocks ? render_kernel<false, kPrimsBlocks> : render_kernel<false, kPrimsModels>);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, C, R, accum, segcount,
+                       counter, stats);
     return hipGetLastError();
 }
 
@@ -2262,7 +2367,7 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
                             unsigned long long *stats, hipStream_t stream) {
     // refill 0: the adaptive threshold
     void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &stats};
-    const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, extend_lds_bytes(S),
+    const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth),
                                          stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
@@ -2281,7 +2386,9 @@ hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRende
 hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuffers &B, uint32_t q, int grid,
                            unsigned long long *stats, hipStream_t stream) {
     const bool nee = S.sun.sun_sampling != 0;
-    const void *fn = S.has_models ? (nee ? reinterpret_cast<const void *>(wf_drain_kernel<kPrimsModels, true>)
+    const void *fn = S.has_blocks ? (nee ? reinterpret_cast<const void *>(wf_drain_kernel<kPrimsBlocks, true>)
+                                         : reinterpret_cast<const void *>(wf_drain_kernel<kPrimsBlocks, false>))
+                     : S.has_models ? (nee ? reinterpret_cast<const void *>(wf_drain_kernel<kPrimsModels, true>)
                                          : reinterpret_cast<const void *>(wf_drain_kernel<kPrimsModels, false>))
                      : S.has_cuboids ? (nee ? reinterpret_cast<const void *>(wf_drain_kernel<kPrimsBoxes, true>)
                                             : reinterpret_cast<const void *>(wf_drain_kernel<kPrimsBoxes, false>))
@@ -2302,11 +2409,11 @@ hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t 
 
 hipError_t launch_intersect(const DevScene &S0, const float *rays, const uint32_t *last_prim, const float *last_normal,
                             uint32_t n, float *t, uint32_t *prim, float *normal, uint32_t *steps, hipStream_t stream) {
-    DevScene S = S0;
-    S.n_cached = 0;  // only wf_extend_kernel mirrors the top slots in LDS
+    const DevScene &S = S0;
     const uint32_t grid = (n + kBlock - 1u) / kBlock;
-    hipLaunchKernelGGL(intersect_kernel, dim3(grid), dim3(kBlock), render_lds_bytes(S.depth), stream, S, rays,
-                       last_prim, last_normal, n, t, prim, normal, steps);
+    hipLaunchKernelGGL(S.has_blocks ? intersect_kernel<kPrimsBlocks> : intersect_kernel<kPrimsModels>, dim3(grid),
+                       dim3(kBlock), render_lds_bytes(S.depth), stream, S, rays, last_prim, last_normal, n, t, prim,
+                       normal, steps);
     return hipGetLastError();
 }
 

@@ -83,8 +83,9 @@ class HipRenderer:
     """RenderingBackend implemented on one MI355X (HIP device `device`)."""
 
     def __init__(self, device: int = 0, resolution=(500, 500), target_spp: int = 1, seed: int = 1,
-                 max_depth: int = 5):
-        self._lib = _lib.load()
+                 max_depth: int = 5, lib_path=None):
+        # lib_path: another build of the same ABI (bench.py's issued-bytes diagnostic library)
+        self._lib = _lib.load(lib_path) if lib_path else _lib.load()
         ctx = C.c_void_p()
         st = self._lib.octpt_create(int(device), C.byref(ctx))
         if st != _lib.OK:

@@ -209,14 +209,23 @@ class Scene:
     quads: np.ndarray = field(default_factory=lambda: np.zeros(0, _lib.QUAD_DTYPE))
     f_sub_surface: float = 0.3  # Scene::f_sub_surface (scene/mod.rs:152), used by sun sampling (path_tracer.rs:240)
     octree: Octree | None = None
+    # block-value leaves: the octree's leaf payloads are block ids into `blocks` (six face
+    # materials per block, Face order W,E,Bottom,Top,South,North), block_model[b] = MODEL_NONE (the block
+    # fills its leaf cell) or a block model; `cells` (n, 4) = (x, y, z, block) the builder voxelises
+    blocks: np.ndarray | None = None
+    block_model: np.ndarray | None = None
+    cells: np.ndarray | None = None
 
     # ---------------------------------------------------------------- octree
     def build_octree(self, depth: int, renderer=None, compact: bool = False) -> Octree:
         """Voxelise the primitives with the product builder: octpt_build_octree (host), or with a
         HipRenderer given, octpt_build_octree_device on its GPU (the same arrays).  compact: merge
         eight sibling leaves holding the same primitive list, bottom-up (OCTPT_BUILD_COMPACT,
-        Octant::is_compactable, new_octree.rs:227-233)."""
+        Octant::is_compactable, new_octree.rs:227-233).  A block-value scene (C23) builds from its
+        cells with octpt_build_block_octree (compact: eight equal block values merge)."""
         lib = _lib.load()
+        if self.blocks is not None:
+            return self._build_block_octree(lib, depth, compact)
         sph = self.sphere_structs()
         cub = self.cuboid_structs()
         handle = C.c_void_p()
@@ -246,6 +255,34 @@ class Scene:
         finally:
             lib.octpt_octree_free(handle)
         return self.octree
+
+    def _build_block_octree(self, lib, depth: int, compact: bool) -> Octree:
+        cells = np.ascontiguousarray(self.cells, np.uint32).reshape(-1, 4)
+        handle = C.c_void_p()
+        _lib.check(lib, None, lib.octpt_build_block_octree(cells.ctypes.data_as(C.c_void_p) if len(cells) else None,
+                                                           len(cells), depth, _lib.BUILD_COMPACT if compact else 0,
+                                                           C.byref(handle)))
+        try:
+            v = _lib.OctreeView()
+            _lib.check(lib, None, lib.octpt_octree_get_view(handle, C.byref(v)))
+            dt = np.dtype([("m", "<u2"), ("r", "<u2"), ("c", "<u4", (8,))])
+            raw = np.ctypeslib.as_array(C.cast(v.octants, C.POINTER(C.c_uint8)), shape=(36 * v.octant_count,))
+            oct_ = raw.view(dt)
+            z = np.zeros(0, np.uint32)
+            self.octree = Octree(oct_["m"].copy(), oct_["c"].copy(), int(v.root), int(v.depth), z, z.copy(), z.copy())
+        finally:
+            lib.octpt_octree_free(handle)
+        return self.octree
+
+    def block_structs(self):
+        """octpt_block rows of `blocks` / `block_model` (C23)."""
+        n = len(self.blocks)
+        arr = (_lib.Block * max(n, 1))()
+        buf = np.frombuffer(arr, dtype=np.dtype([("f", "<u4", (6,)), ("m", "<u4"), ("r", "<u4")]))
+        buf["f"][:n] = np.asarray(self.blocks, np.uint32).reshape(-1, 6)
+        buf["m"][:n] = (self.block_model if self.block_model is not None
+                        else np.full(n, _lib.MODEL_NONE, np.uint32))
+        return arr
 
     # ---------------------------------------------------------------- ABI views
     def sphere_structs(self):
@@ -336,16 +373,19 @@ class Scene:
         desc.sun = self.sun_struct()
         desc.emitters_enabled = int(self.emitters_enabled)
         desc.f_sub_surface = self.f_sub_surface
-        if self.cuboid_model is not None and len(self.cuboids):
-            cmod = np.ascontiguousarray(self.cuboid_model, np.uint32)
+        if (self.cuboid_model is not None and len(self.cuboids)) or self.blocks is not None:
             mdl = np.zeros((max(len(self.models), 1), 4), np.uint32)
             mdl[: len(self.models), 1:3] = np.asarray(self.models, np.uint32).reshape(-1, 2)
             qd = np.ascontiguousarray(self.quads)
-            desc.cuboid_model = ptr(cmod)
-            desc.models = ptr(mdl)
+            if self.cuboid_model is not None and len(self.cuboids):
+                desc.cuboid_model = ptr(np.ascontiguousarray(self.cuboid_model, np.uint32))
+            desc.models = ptr(mdl) if len(self.models) else None
             desc.model_count = len(self.models)
             desc.quads = ptr(qd) if len(qd) else None
             desc.quad_count = len(qd)
+        if self.blocks is not None:  # block-value leaves (C23)
+            desc.blocks = ptr(self.block_structs())
+            desc.block_count = len(self.blocks)
         keep.extend([mats, texs])
         return desc, keep
 
@@ -680,6 +720,59 @@ def terrain_tops(seed: int, side: int, origin: int = 24) -> np.ndarray:
     return np.stack([xx.ravel() + origin, hmap.astype(np.int64).ravel(), zz.ravel() + origin], 1)
 
 
+def voxels_to_blocks(scene: Scene) -> Scene:
+    """The same world with block-value leaves, the reference's own leaf form: every
+    unit-voxel cuboid [x, x+1)^3 becomes a cell whose leaf value is a block id; blocks are the distinct
+    (six face materials, block model) rows.  Materials, textures, models, quads, sun and strategy are
+    shared with `scene`; the octree is built by build_octree (octpt_build_block_octree)."""
+    cub = np.asarray(scene.cuboids, F32).reshape(-1, 6)
+    lo = cub[:, :3]
+    if not (np.all(cub[:, 3:] == lo + F32(1.0)) and np.all(lo == np.floor(lo)) and np.all(lo >= 0)):
+        raise ValueError("voxels_to_blocks: every cuboid must be a unit voxel [x, x+1)^3 at integer x >= 0")
+    model = (np.asarray(scene.cuboid_model, np.uint32) if scene.cuboid_model is not None
+             else np.full(len(cub), _lib.MODEL_NONE, np.uint32))
+    fm = np.asarray(scene.cuboid_material, np.uint32).reshape(-1, 6).copy()
+    fm[model != _lib.MODEL_NONE] = 0  # a model block's faces come from its quads
+    rows = np.concatenate([fm, model[:, None]], 1)
+    table, inv = np.unique(rows, axis=0, return_inverse=True)
+    out = Scene(materials=scene.materials, textures=scene.textures, sun=scene.sun, strategy=scene.strategy,
+                emitters_enabled=scene.emitters_enabled, models=scene.models, quads=scene.quads,
+                f_sub_surface=scene.f_sub_surface)
+    out.blocks = np.ascontiguousarray(table[:, :6], np.uint32)
+    out.block_model = np.ascontiguousarray(table[:, 6], np.uint32)
+    out.cells = np.concatenate([lo.astype(np.uint32), inv.reshape(-1, 1).astype(np.uint32)], 1)
+    return out
+
+
+def solid_terrain(scene: Scene, seed: int, side: int, origin: int = 24, floor: int = 0):
+    """A block-value world on voxel_terrain's heightmap, every column solid from `floor`
+    to its top -- the shape of a Minecraft region, whose underground compacts into LOD leaves (the
+    section builder's Lod(section_fill_block) and RegionOctreeBuilder's Lod(data), new_octree.rs:534-537,
+    586, 727).  Blocks: 0 grass, 1 dirt, 2 stone, 3 snow, 4 sand (voxel_terrain's face materials); the top
+    block by height as there, three dirt below it, stone beneath.  Sets scene.blocks / cells."""
+    mat = block_materials(scene, seed)
+    scene.blocks = np.array([[mat["grass_side"]] * 2 + [mat["dirt"], mat["grass_top"]] + [mat["grass_side"]] * 2,
+                             [mat["dirt"]] * 6, [mat["stone"]] * 6,
+                             [mat["snow_side"]] * 2 + [mat["dirt"], mat["snow"]] + [mat["snow_side"]] * 2,
+                             [mat["sand"]] * 6], np.uint32)
+    scene.block_model = np.full(5, _lib.MODEL_NONE, np.uint32)
+    h = (48 + np.floor(128 * _value_noise(seed, 400, side, side, [(6, 6), (12, 12), (24, 24), (48, 48)]))).astype(
+        np.int64).ravel()
+    count = h - floor + 1
+    col = np.repeat(np.arange(side * side, dtype=np.int64), count)
+    first = np.repeat(np.cumsum(count) - count, count)
+    below = np.arange(len(col), dtype=np.int64) - first  # 0 = the top block
+    top = h[col]
+    kind = np.where(below >= 4, 2, np.where(below >= 1, 1, np.where(top >= 150, 3, np.where(top < 64, 4, 0))))
+    cells = np.empty((len(col), 4), np.uint32)
+    cells[:, 0] = col % side + origin
+    cells[:, 1] = top - below
+    cells[:, 2] = col // side + origin
+    cells[:, 3] = kind
+    scene.cells = cells
+    return scene
+
+
 def _assign_materials(ids, seed, n, stream=7):
     """70% diffuse, 15% metal, 10% glossy, 5% glass."""
     u = scene_uniform(seed, stream, n)
@@ -705,14 +798,42 @@ def random_cuboids(seed: int, n: int, world: float, emin: float, emax: float):
     return np.concatenate([lo, np.minimum(lo + ext, F32(world - 0.001))], axis=1).astype(F32)
 
 
-CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny", "blocks", "C3-in", "C5-fp")
+CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny", "blocks", "C3-in", "C5-fp", "C5b", "C5b-fp", "blocks-b",
+           "C5s", "C5s-fp", "C5s-small")
 
 
 C5_SIDE = 1000  # columns per side: 1,001,225 unit blocks with the exposed-side fill
 
 
 def make_config(name: str, *, seed: int = 1, build: bool = True):
-    """(Scene, Camera, RenderSettings) for BASELINE.json's configs."""
+    """(Scene, Camera, RenderSettings) for BASELINE.json's configs.  A "b" suffix
+    (C5b, C5b-fp, blocks-b) is the same voxel world with block-value leaves."""
+    if name in ("C5b", "C5b-fp", "blocks-b"):
+        base = {"C5b": "C5", "C5b-fp": "C5-fp", "blocks-b": "blocks"}[name]
+        sc, cam, rs = make_config(base, seed=seed, build=False)
+        sb = voxels_to_blocks(sc)
+        depth = sc._depth  # type: ignore[attr-defined]
+        if build:
+            sb.build_octree(depth)
+        else:
+            sb._depth = depth  # type: ignore[attr-defined]
+        return sb, cam, rs
+    if name in ("C5s", "C5s-fp", "C5s-small"):
+        # C5's heightmap as a solid block-value world (C23); C5s-small: 128 x 128 columns (tests)
+        sc = Scene()
+        side = 128 if name == "C5s-small" else C5_SIDE
+        solid_terrain(sc, seed, side)
+        depth = 11
+        mid = 24 + side / 2
+        cam = Camera.look_at((mid, 230.0, 24.0 - 60.0 * side / C5_SIDE), (mid, 100.0, mid))
+        if name == "C5s-fp":
+            cam = Camera.look_at((300.5, 190.0, 300.5), (800.0, 120.0, 800.0))
+        rs = RenderSettings(3840, 2160, 1024, seed=seed)
+        if build:
+            sc.build_octree(depth)
+        else:
+            sc._depth = depth  # type: ignore[attr-defined]
+        return sc, cam, rs
     sc = Scene()
     if name in ("C1", "C1-as-is"):
         ids = primitive_materials(sc)

@@ -385,7 +385,7 @@ static inline float inv_clamped(float d) { return fabsf(d) < 1e-6f ? 1.0f / 1e-6
 /* ------------------------------------------------------------------------- */
 /* textures, src/textures/texture.rs:64-93 (+ rtw_image.rs:234-237, [C9])       */
 /* ------------------------------------------------------------------------- */
-static void texture_value(ctx_t *c, uint32_t tex_idx, float u, float v, float out[4]) {
+static void texture_value_n(ctx_t *c, uint32_t tex_idx, float u, float v, float out[4], int count) {
     const ref_scene *s = c->s;
     const ref_texture *t = &s->textures[tex_idx];
     if (t->kind == 0) { tex_value_color(t->rgba, out); return; }
@@ -398,11 +398,14 @@ static void texture_value(ctx_t *c, uint32_t tex_idx, float u, float v, float ou
     if (i > t->width - 1) i = t->width - 1;
     if (j > t->height - 1) j = t->height - 1;
     const uint8_t *px = s->texels + t->offset + ((uint64_t)j * t->width + i) * 4u;
-    c->st.texel_reads++;
+    if (count) c->st.texel_reads++;
     out[0] = LUT_FLOAT[px[0]];
     out[1] = LUT_FLOAT[px[1]];
     out[2] = LUT_FLOAT[px[2]];
     out[3] = (float)px[3] / 255.0f;
+}
+static void texture_value(ctx_t *c, uint32_t tex_idx, float u, float v, float out[4]) {
+    texture_value_n(c, tex_idx, u, v, out, 1);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -415,6 +418,9 @@ typedef struct {
     v3 n;        /* outward normal */
     int64_t quad;        /* block-model hit: the global quad index, else -1 [C19] */
     float alpha, beta;   /* its Quad::hit barycentrics */
+    int64_t block;       /* block-value leaf hit [C23]: the block id, else -1 */
+    int face;            /* its face (Face enum index) */
+    float u, v;          /* its texture coordinates (octree_traversal.rs:159-190, |u|, |v|) */
 } prim_hit;
 
 /* Sphere::hit dead code after todo!() (geometry/sphere.rs:33-57) + [C2] root selection */
@@ -517,9 +523,7 @@ static int quad_hit(const quad_geo *g, const ray_t *r, v3 voxel, float t_next, f
 /* a block-model leaf (ResourceModel::Quad, octree_traversal.rs:207-213) [C19]: the closest of the
  * model's quads with 0 < t <= t_accept, ties to the later quad (`t > t_next` rejects), skipping
  * the quad the ray leaves */
-static int model_test(const ref_scene *s, const ray_t *r, uint32_t ci, uint32_t mdl, float t_accept, prim_hit *h) {
-    const float *bx = &s->cuboids[6 * (size_t)ci];
-    v3 voxel = V(bx[0], bx[1], bx[2]);
+static int model_test_at(const ref_scene *s, const ray_t *r, v3 voxel, uint32_t mdl, float t_accept, prim_hit *h) {
     uint32_t first = s->model_quads[2 * (size_t)mdl], cnt = s->model_quads[2 * (size_t)mdl + 1];
     float t_next = t_accept;
     int found = 0;
@@ -542,6 +546,10 @@ static int model_test(const ref_scene *s, const ray_t *r, uint32_t ci, uint32_t 
     h->axis = 0;
     return found;
 }
+static int model_test(const ref_scene *s, const ray_t *r, uint32_t ci, uint32_t mdl, float t_accept, prim_hit *h) {
+    const float *bx = &s->cuboids[6 * (size_t)ci];
+    return model_test_at(s, r, V(bx[0], bx[1], bx[2]), mdl, t_accept, h);
+}
 
 /* Face enum index from outward normal (geometry/cuboid.rs:9-29) */
 static inline int face_index(int axis, float sgn) {
@@ -557,7 +565,13 @@ static void commit_hit(ctx_t *c, ray_t *r, uint32_t prim, const prim_hit *h) {
     float u, v;
     uint32_t mat;
     v3 n;
-    if (h->quad >= 0) { /* block-model quad [C19]: uv from the barycentrics (quad.rs:194-197) */
+    if (h->block >= 0 && h->quad < 0) { /* a block filling its leaf cell [C23]: face and uv from ESVO */
+        n = h->n;
+        u = h->u;
+        v = h->v;
+        mat = s->block_mat[6 * (size_t)h->block + (size_t)h->face];
+        prim = PRIM_NONE; /* no self-intersection key: a ray starting in a block's cell skips it (t_min == 0) */
+    } else if (h->quad >= 0) { /* block-model quad [C19]: uv from the barycentrics (quad.rs:194-197) */
         const ref_quad *q = &s->quads[h->quad];
         n = h->n;
         u = q->texture_u_range[0] + h->alpha * (q->texture_u_range[1] - q->texture_u_range[0]);
@@ -634,6 +648,7 @@ static int leaf_test(ctx_t *c, const ray_t *r, uint32_t leaf, float t_exit_w, fl
         int ok;
         c->st.prim_tests++;
         h.quad = -1;
+        h.block = -1;
         uint32_t mdl = (prim & PRIM_CUBOID_BIT) && s->cuboid_model ? s->cuboid_model[prim & ~PRIM_CUBOID_BIT] : MODEL_NONE;
         if (!(prim & PRIM_CUBOID_BIT)) ok = sphere_test(&s->spheres[4 * (size_t)prim], r, self_prim, &h);
         else if (mdl != MODEL_NONE) ok = model_test(s, r, prim & ~PRIM_CUBOID_BIT, mdl, t_accept, &h);
@@ -645,6 +660,78 @@ static int leaf_test(ctx_t *c, const ray_t *r, uint32_t leaf, float t_exit_w, fl
         }
     }
     return found;
+}
+
+/* A block-value leaf [C23]: the leaf payload is a block id and the block's box is the leaf cell itself,
+ * at any level (the reference's own leaf form: new_octree.rs:534-537, 586, 669, 727).  Restates the
+ * leaf arm of intersect_octree_path_tracer (octree_traversal.rs:143-214) from its ESVO state:
+ *  - the unmirrored cell corner (:149-154) and the cell's entry t-values at pos + scale_exp2 (:156);
+ *  - the face is the axis of their maximum, UV the entry point's other two coordinates over the cell
+ *    (:159-190), flipped where the ray runs negative; |u|, |v| as Cuboid::intersect_texture
+ *    (cuboid.rs:73-90).  The face id :164 is written 1 << 0 | sign for X, which always names East: the
+ *    pattern of :173 / :182 (2 * axis + sign) is taken for all three axes, like the RGBA stride of C9;
+ *  - ResourceModel::SingleBlock (:193-206): skipped when t_min == 0 (the ray starts inside the cell: the
+ *    next block's face, not this one's, is hit), else SingleBlockModel::intersect -- undefined in the
+ *    reference -- is the face material's texel at (u, v): a hit unless its alpha <= EPSILON (a
+ *    transparent texel: ESVO advances, :215), hit t = t_min / octree_scale (:197);
+ *  - ResourceModel::Quad (:207-213): the block's model (C19) at the cell's world corner
+ *    ((pos - 1) / octree_scale, unit-voxel quads), closest quad before the cell exit + tolerance (C1). */
+static int block_leaf_test(ctx_t *c, const ray_t *r, uint32_t block, v3 pos, float scale_exp2, v3 ro, v3 rd,
+                           v3 t_coef, v3 t_bias, uint32_t mirror, float t_min, float tc_max, prim_hit *h) {
+    const ref_scene *s = c->s;
+    const float octree_scale = c->octree_scale;
+    c->st.leaf_visits++;
+    c->st.block_tests++;
+    v3 upos = pos; /* :149-154 */
+    for (int i = 0; i < 3; i++)
+        if (mirror & (1u << i)) vset(&upos, i, (3.0f - scale_exp2) - vget(pos, i));
+    h->quad = -1;
+    h->block = block;
+    const uint32_t mdl = s->block_model ? s->block_model[block] : MODEL_NONE;
+    if (mdl != MODEL_NONE) { /* :207-213 */
+        v3 voxel = V((upos.x - 1.0f) / octree_scale, (upos.y - 1.0f) / octree_scale, (upos.z - 1.0f) / octree_scale);
+        float t_accept = tc_max / octree_scale + CELL_TOL * (scale_exp2 / octree_scale);
+        return model_test_at(s, r, voxel, mdl, t_accept, h);
+    }
+    if (t_min == 0.0f) return 0; /* :194 */
+    const float se = scale_exp2;
+    v3 tcn = vsub(vmul(vadd(pos, V(se, se, se)), t_coef), t_bias); /* :156 */
+    float tc_min = vmax3(tcn);
+    int axis;
+    float u, v;
+    if (tcn.x == tc_min) { /* :163-171 */
+        axis = 0;
+        u = ((ro.z + rd.z * tcn.x) - upos.z) / se;
+        v = ((ro.y + rd.y * tcn.x) - upos.y) / se;
+        if (rd.x < 0.0f) u = 1.0f - u;
+    } else if (tcn.y == tc_min) { /* :172-180 */
+        axis = 1;
+        u = ((ro.x + rd.x * tcn.y) - upos.x) / se;
+        v = ((ro.z + rd.z * tcn.y) - upos.z) / se;
+        if (rd.y < 0.0f) v = 1.0f - v;
+    } else { /* :181-189 */
+        axis = 2;
+        u = ((ro.x + rd.x * tcn.z) - upos.x) / se;
+        v = ((ro.y + rd.y * tcn.z) - upos.y) / se;
+        if (rd.z < 0.0f) u = 1.0f - u;
+    }
+    u = fabsf(u);
+    v = fabsf(v);
+    const float sgn = vget(rd, axis) < 0.0f ? 1.0f : -1.0f; /* the face the ray enters faces against it */
+    const int face = face_index(axis, sgn);
+    const uint32_t mat = s->block_mat[6 * (size_t)block + (size_t)face];
+    float col[4];
+    texture_value_n(c, s->materials[mat].texture_index, u, v, col, 0); /* the alpha test reads no counted texel */
+    if (!(col[3] > RAY_EPSILON)) return 0;
+    h->t = t_min / octree_scale;
+    h->inside = 0;
+    h->axis = axis;
+    h->n = V(0.0f, 0.0f, 0.0f);
+    vset(&h->n, axis, sgn);
+    h->face = face;
+    h->u = u;
+    h->v = v;
+    return 1;
 }
 
 #ifdef REF_ESVO_TRACE
@@ -726,7 +813,12 @@ static int esvo(ctx_t *c, const ray_t *ray, float max_dst_w, uint32_t *hit_prim,
             if (is_leaf && t_min >= 0.0f) {                                /* :143 */
                 float cell_w = scale_exp2 / octree_scale;
                 tcode = 1;
-                if (leaf_test(c, ray, payload, tc_max / octree_scale, cell_w, hit_prim, hit)) {
+                int found = s->block_mat
+                                ? block_leaf_test(c, ray, payload, pos, scale_exp2, ro, rd, t_coef, t_bias, mirror,
+                                                  t_min, tc_max, hit)
+                                : leaf_test(c, ray, payload, tc_max / octree_scale, cell_w, hit_prim, hit);
+                if (found && s->block_mat) *hit_prim = payload;
+                if (found) {
                     TRACE(2);
                     *steps_out = steps;
                     return 1;
@@ -1381,6 +1473,7 @@ static void *render_worker(void *arg) {
     j->total.leaf_visits += c.st.leaf_visits;
     j->total.shade_events += c.st.shade_events;
     j->total.texel_reads += c.st.texel_reads;
+    j->total.block_tests += c.st.block_tests;
     if (c.st.max_path_segs > j->total.max_path_segs) j->total.max_path_segs = c.st.max_path_segs;
     pthread_mutex_unlock(&j->lock);
     return NULL;
@@ -1526,7 +1619,8 @@ void ref_intersect(const ref_scene *s, const float *rays, const uint32_t *last_p
         if (hit) {
             commit_hit(&c, &r, prim, &h);
             out_t[i] = h.t;
-            out_prim[i] = prim;
+            /* block-value scenes [C23]: the block id, or QUAD_KEY | quad for a block model's quad */
+            out_prim[i] = (s->block_mat && h.quad >= 0) ? (QUAD_KEY | (uint32_t)h.quad) : prim;
             if (out_normal) { out_normal[3 * i] = r.n.x; out_normal[3 * i + 1] = r.n.y; out_normal[3 * i + 2] = r.n.z; }
         } else {
             out_t[i] = INFINITY;

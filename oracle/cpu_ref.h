@@ -106,6 +106,14 @@ typedef struct {
     uint32_t n_models;
     const ref_quad *quads;
     uint32_t n_quads;
+    /* block-value leaves: block_mat non-NULL = every leaf payload is a block id, the
+     * reference's own leaf form (new_octree.rs:534-537, 586, 669, 727).  Block b has the face materials
+     * block_mat[6b .. 6b+5] (Face order W,E,Bottom,Top,South,North) and block_model[b] (NULL or
+     * 0xFFFFFFFF: the block fills its leaf cell, the SingleBlock arm of octree_traversal.rs:143-205;
+     * else a block model drawn at the cell's corner, the ResourceModel::Quad arm :207-213) */
+    const uint32_t *block_mat;
+    const uint32_t *block_model;
+    uint32_t n_blocks;
 } ref_scene;
 
 typedef struct {
@@ -125,6 +133,7 @@ typedef struct {
 typedef struct {
     uint64_t paths, segments, esvo_steps, node_fetches, prim_tests, leaf_visits, shade_events, texel_reads;
     uint64_t max_path_segs;
+    uint64_t block_tests; /* block-value leaf tests [C23] */
 } ref_stats;
 
 /* --- math --- */

@@ -54,7 +54,8 @@ class RefScene(C.Structure):
                 ("n_materials", C.c_uint32), ("textures", C.c_void_p), ("n_textures", C.c_uint32),
                 ("texels", C.c_void_p), ("sun", RefSun), ("emitters_enabled", C.c_int32),
                 ("f_sub_surface", C.c_float), ("cuboid_model", C.c_void_p), ("model_quads", C.c_void_p),
-                ("n_models", C.c_uint32), ("quads", C.c_void_p), ("n_quads", C.c_uint32)]
+                ("n_models", C.c_uint32), ("quads", C.c_void_p), ("n_quads", C.c_uint32),
+                ("block_mat", C.c_void_p), ("block_model", C.c_void_p), ("n_blocks", C.c_uint32)]
 
 
 class RefParams(C.Structure):
@@ -66,7 +67,8 @@ class RefParams(C.Structure):
 
 class RefStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("paths", "segments", "esvo_steps", "node_fetches", "prim_tests",
-                                           "leaf_visits", "shade_events", "texel_reads", "max_path_segs")]
+                                           "leaf_visits", "shade_events", "texel_reads", "max_path_segs",
+                                           "block_tests")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -215,15 +217,22 @@ class OracleScene:
                           len(sp), _p(cb), _p(cm), len(cb), C.cast(mats, C.c_void_p), len(scene.materials),
                           C.cast(texs, C.c_void_p), len(scene.textures), _p(texels), sun, int(scene.emitters_enabled),
                           scene.f_sub_surface)
-        if scene.cuboid_model is not None and len(scene.cuboids):
-            self.s.cuboid_model = _p(k(scene.cuboid_model, np.uint32))
+        blocks = getattr(scene, "blocks", None)
+        if (scene.cuboid_model is not None and len(scene.cuboids)) or blocks is not None:
+            if scene.cuboid_model is not None and len(scene.cuboids):
+                self.s.cuboid_model = _p(k(scene.cuboid_model, np.uint32))
             mq = k(np.asarray(scene.models, np.uint32).reshape(-1, 2), np.uint32)
             self.s.model_quads = _p(mq)
             self.s.n_models = len(mq)
             qd = np.ascontiguousarray(scene.quads)
             self._keep.append(qd)
-            self.s.quads = qd.ctypes.data
+            self.s.quads = qd.ctypes.data if len(qd) else None
             self.s.n_quads = len(qd)
+        if blocks is not None:  # block-value leaves
+            self.s.block_mat = _p(k(np.asarray(blocks, np.uint32).reshape(-1, 6), np.uint32))
+            bm = scene.block_model if scene.block_model is not None else np.full(len(blocks), 0xFFFFFFFF, np.uint32)
+            self.s.block_model = _p(k(bm, np.uint32))
+            self.s.n_blocks = len(blocks)
 
 
 def render(scene, camera, width, height, spp, *, spp_start=0, max_depth=5, seed=1, threads=8, forward=False,

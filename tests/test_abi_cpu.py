@@ -19,7 +19,9 @@ STRUCTS = {"octpt_octant": "Octant", "octpt_sphere": "Sphere", "octpt_cuboid": "
            "octpt_material": "Material", "octpt_texture": "Texture", "octpt_sun": "Sun",
            "octpt_scene_desc": "SceneDesc", "octpt_camera": "Camera", "octpt_render_params": "RenderParams",
            "octpt_stats": "Stats", "octpt_octree_view": "OctreeView", "octpt_quad": "Quad",
-           "octpt_block_model": "BlockModel"}
+           "octpt_block_model": "BlockModel", "octpt_block": "Block",
+           "octpt_reference_material": "ReferenceMaterial", "octpt_reference_quad": "ReferenceQuad",
+           "octpt_reference_scene": "ReferenceScene"}
 
 
 def header_functions():
@@ -73,7 +75,7 @@ def test_reference_layout_sizes():
 
 
 def test_version_and_devices(lib):
-    assert lib.octpt_abi_version() == _lib.OCTPT_ABI_VERSION == 2
+    assert lib.octpt_abi_version() == _lib.OCTPT_ABI_VERSION == 3
     assert lib.octpt_device_count() >= 0
 
 

@@ -1,0 +1,237 @@
+"""Block-value leaves on the CPU: the block octree builder, the reference's section
+builder restated (tests/reference_builders.py), the oracle's block leaf test against an independent
+voxel DDA, and the reference-scene flattener (octpt_scene_from_reference) -- no GPU."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from octree_pathtracing_amd import _lib
+from octree_pathtracing_amd import scene as S
+from tests import reference_builders as RB
+
+
+def random_section(seed: int, air: float = 0.45, kinds: int = 5) -> np.ndarray:
+    """16^3 blocks, `air` of them empty, a few solid runs so that compaction has work."""
+    rng = np.random.default_rng(seed)
+    g = rng.integers(1, kinds + 1, size=(16, 16, 16)).astype(np.uint32)
+    g[rng.random((16, 16, 16)) < air] = 0
+    g[:8, :4, :8] = 2      # a solid 8x4x8 run of one block: LOD leaves at levels 1 and 2
+    g[8:, 12:, 8:] = 0     # an empty corner
+    return g
+
+
+def block_scene(grid: np.ndarray, depth: int, compact: bool, origin=(0, 0, 0)) -> S.Scene:
+    sc = S.Scene()
+    mat = S.block_materials(sc, 7)
+    names = list(S.BLOCK_TILES)
+    n = int(grid.max())
+    sc.blocks = np.array([[mat[names[(b + f) % len(names)]] for f in range(6)] for b in range(n + 1)], np.uint32)
+    sc.block_model = np.full(n + 1, _lib.MODEL_NONE, np.uint32)
+    xyz = np.argwhere(grid > 0)
+    sc.cells = np.concatenate([xyz + np.asarray(origin), grid[tuple(xyz.T)][:, None]], 1).astype(np.uint32)
+    sc.build_octree(depth, compact=compact)
+    return sc
+
+
+def leaf_levels(t: S.Octree) -> dict:
+    """level of every leaf child (0 = a unit cell) -> count, walking from the root (C21 encodings)."""
+    out = {}
+
+    def walk(node, level):
+        m = int(t.octant_mask[node])
+        for i in range(8):
+            present, high = (m >> i) & 1, (m >> (i + 8)) & 1
+            if present and high:
+                out[level - 1] = out.get(level - 1, 0) + 1
+            elif present or high:
+                walk(int(t.octant_children[node, i]), level - 1)
+
+    walk(t.root, t.depth)
+    return out
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_block_builder_decodes_every_cell(compact):
+    g = random_section(1)
+    grid = np.zeros((32, 32, 32), np.uint32)
+    grid[8:24, 4:20, 16:32] = g
+    sc = block_scene(grid, 5, compact)
+    t = sc.octree
+    for x, y, z in np.ndindex(*grid.shape):
+        assert RB.decode_cell(t.octant_mask, t.octant_children, t.root, t.depth, x, y, z) == grid[x, y, z]
+    lv = leaf_levels(t)
+    if compact:  # the solid run merges into LOD leaves at levels >= 1 (is_compactable, new_octree.rs:227-233)
+        assert lv.get(2, 0) > 0 and sum(v for k, v in lv.items() if k >= 1) >= 4
+        # no octant below the root keeps eight equal leaves
+        for node in range(t.octant_count):
+            m = int(t.octant_mask[node])
+            if node != t.root and m == 0xFFFF:
+                assert len(set(t.octant_children[node].tolist())) > 1
+    else:
+        assert set(lv) == {0}
+
+
+def test_block_builder_rejects_bad_cells():
+    lib = _lib.load()
+    out = C.c_void_p()
+
+    def build(cells, depth=4):
+        a = np.ascontiguousarray(cells, np.uint32).reshape(-1, 4)
+        return lib.octpt_build_block_octree(a.ctypes.data_as(C.c_void_p), len(a), depth, 0, C.byref(out))
+
+    assert build([[1, 2, 3, 4], [1, 2, 3, 5]]) == _lib.ERR_INVALID_ARG      # two blocks in one cell
+    assert build([[16, 0, 0, 1]]) == _lib.ERR_INVALID_ARG                  # outside [0, 2^depth)
+    assert build([[0, 0, 0, 1 << 27]]) == _lib.ERR_INVALID_ARG             # block id >= 2^27
+    assert build([[1, 2, 3, 4]], depth=0) == _lib.ERR_INVALID_ARG
+    assert build([[1, 2, 3, 4]]) == _lib.OK
+    lib.octpt_octree_free(out)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_section_builder_restatement(seed):
+    """tests/reference_builders.section_octants (SectionOctantBuilder, new_octree.rs:599-710): the
+    writer's encoding, root 0, and every cell decodes to its block."""
+    g = random_section(seed)
+    kind, masks, children = RB.section_octants(g)
+    assert kind == "subtree"
+    assert np.all((masks & 0xFF) & ~(masks >> 8) == 0)  # writer form: bit i implies bit i + 8
+    assert np.any((masks >> 8) & ~(masks & 0xFF))      # octant children carry bit i + 8 alone
+    for x, y, z in np.ndindex(16, 16, 16):
+        assert RB.decode_cell(masks, children, 0, 4, x, y, z) == g[x, y, z]
+    # its compaction agrees with the product builder's: the same number of octants
+    sc = block_scene(g, 4, True)
+    assert sc.octree.octant_count == len(masks)
+
+
+def test_section_builder_lod_and_empty():
+    assert RB.section_octants(np.full((16, 16, 16), 3, np.uint32)) == ("lod", 3)      # Lod(section_fill_block)
+    assert RB.section_octants(np.zeros((16, 16, 16), np.uint32)) == ("empty", 0)
+
+
+def test_morton_restatement_matches_oracle():
+    from oracle import cpu_ref
+
+    lib = cpu_ref.load()
+    for x, y, z in [(1, 0, 1), (15, 3, 7), (1023, 1023, 1023), (5, 900, 17)]:
+        assert RB.encode_morton(x, y, z) == lib.ref_morton_encode(x, y, z)
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_oracle_block_hits_match_voxel_dda(compact):
+    """The oracle's block leaf test (oracle/cpu_ref.c block_leaf_test, octree_traversal.rs:143-205)
+    against an independent float64 voxel DDA: the first block a ray enters, the face axis and t."""
+    from oracle import cpu_ref
+
+    g = random_section(4, air=0.85)
+    sc = block_scene(g, 4, compact)
+    rng = np.random.default_rng(9)
+    n = 400
+    o = rng.uniform(-6.0, 22.0, (n, 3)).astype(np.float32)
+    side = rng.integers(0, 3, n)
+    o[np.arange(n), side] = np.where(rng.random(n) < 0.5, -3.0, 19.0)  # outside the cube on one axis
+    target = rng.uniform(0.5, 15.5, (n, 3)).astype(np.float32)
+    d = target - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d.astype(np.float32)], 1)
+    t, prim, nrm, _ = cpu_ref.intersect(sc, rays)
+    agree = 0
+    for i in range(n):
+        ref = RB.dda_first_block(g, o[i], d[i])
+        if ref is None:
+            assert prim[i] == _lib.PRIM_NONE
+            continue
+        v, axis, tr = ref
+        assert prim[i] == v, i
+        assert abs(t[i] - tr) <= 1e-4 * max(1.0, tr), (i, t[i], tr)
+        assert axis < 0 or abs(nrm[i, axis]) == 1.0
+        agree += 1
+    assert agree > 100
+
+
+def _reference_scene(sc: S.Scene, masks, children, depth, image: bool = True):
+    """An octpt_reference_scene holding `sc`'s materials as the reference's Material + Texture."""
+    keep = []
+    mats = (_lib.ReferenceMaterial * len(sc.materials))()
+    for i, m in enumerate(sc.materials):
+        tx = sc.textures[m.texture_index]
+        mats[i].index_of_refraction, mats[i].specular, mats[i].emittance = m.ior, m.specular, m.emittance
+        mats[i].roughness, mats[i].metalness = m.roughness, m.metalness
+        mats[i].material_flags, mats[i].tint_index = m.flags, m.tint_index
+        mats[i].texture_kind = tx.kind
+        mats[i].color[:] = list(tx.rgba)
+        if tx.kind == _lib.TEXTURE_IMAGE:
+            px = np.ascontiguousarray(tx.pixels, np.uint8)
+            keep.append(px)
+            mats[i].image_width, mats[i].image_height = px.shape[1], px.shape[0]
+            mats[i].image_rgba = px.ctypes.data if image else None
+    octs = (_lib.Octant * len(masks))()
+    buf = np.frombuffer(octs, dtype=np.dtype([("m", "<u2"), ("r", "<u2"), ("c", "<u4", (8,))]))
+    buf["m"], buf["c"] = masks, children
+    blocks = sc.block_structs()
+    ref = _lib.ReferenceScene()
+    ref.octants, ref.octant_count, ref.root, ref.depth = C.cast(octs, C.c_void_p), len(masks), 0, depth
+    ref.blocks, ref.block_count = C.cast(blocks, C.c_void_p), len(sc.blocks)
+    ref.materials, ref.material_count = C.cast(mats, C.c_void_p), len(sc.materials)
+    ref.sun = sc.sun_struct()
+    ref.emitters_enabled, ref.f_sub_surface = 1, 0.3
+    keep += [mats, octs, blocks]
+    return ref, keep
+
+
+def test_scene_from_reference_fills_desc():
+    lib = _lib.load()
+    g = random_section(5)
+    sc = block_scene(g, 4, False)
+    _, masks, children = RB.section_octants(g)
+    ref, keep = _reference_scene(sc, masks, children, 4)
+    n = len(sc.materials)
+    mo, to, qo = (_lib.Material * n)(), (_lib.Texture * n)(), (_lib.Quad * 1)()
+    desc = _lib.SceneDesc()
+    assert lib.octpt_scene_from_reference(C.byref(ref), mo, to, qo, C.byref(desc)) == _lib.OK
+    assert desc.abi_version == _lib.OCTPT_ABI_VERSION and desc.depth == 4 and desc.root == 0
+    assert desc.octant_count == len(masks) and desc.block_count == len(sc.blocks)
+    assert desc.material_count == desc.texture_count == n and desc.quad_count == 0
+    for i, m in enumerate(sc.materials):  # material i with its own texture i (gpu_renderer.rs:221-307)
+        assert mo[i].texture_index == i and mo[i].flags == m.flags and mo[i].ior == np.float32(m.ior)
+        assert to[i].kind == sc.textures[m.texture_index].kind
+    # an image without pixels, or a material index out of range, is refused
+    bad, keep2 = _reference_scene(sc, masks, children, 4, image=False)
+    assert lib.octpt_scene_from_reference(C.byref(bad), mo, to, qo, C.byref(desc)) == _lib.ERR_INVALID_ARG
+    blocks = sc.block_structs()
+    blocks[0].face_material[2] = n
+    ref.blocks = C.cast(blocks, C.c_void_p)
+    assert lib.octpt_scene_from_reference(C.byref(ref), mo, to, qo, C.byref(desc)) == _lib.ERR_INVALID_ARG
+
+
+def test_scene_from_reference_quads():
+    """Box<[Quad]> keeps Quad::new's arguments; a stored normal that is not normalize(u x v) is refused."""
+    lib = _lib.load()
+    sc, _, _ = S.make_config("blocks-b", build=False)
+    rows = sc.quads
+    rq = (_lib.ReferenceQuad * len(rows))()
+    for i, q in enumerate(rows):
+        u, v = q["u"].astype(np.float64), q["v"].astype(np.float64)
+        nn = np.cross(u, v)
+        rq[i].origin[:], rq[i].u[:], rq[i].v[:] = list(q["origin"]), list(q["u"]), list(q["v"])
+        rq[i].normal[:] = list(nn / np.linalg.norm(nn))
+        rq[i].material_id = int(q["material"])
+        rq[i].texture_u_range[:], rq[i].texture_v_range[:] = list(q["texture_u_range"]), list(q["texture_v_range"])
+    g = np.zeros((16, 16, 16), np.uint32)
+    g[2:5, 2, 2:5] = 1
+    _, masks, children = RB.section_octants(g)
+    ref, keep = _reference_scene(sc, masks, children, 4)
+    models = np.zeros((len(sc.models), 4), np.uint32)
+    models[:, 1:3] = sc.models
+    ref.models, ref.model_count = models.ctypes.data, len(models)
+    ref.quads, ref.quad_count = C.cast(rq, C.c_void_p), len(rows)
+    n = len(sc.materials)
+    mo, to, qo = (_lib.Material * n)(), (_lib.Texture * n)(), (_lib.Quad * len(rows))()
+    desc = _lib.SceneDesc()
+    assert lib.octpt_scene_from_reference(C.byref(ref), mo, to, qo, C.byref(desc)) == _lib.OK
+    assert desc.quad_count == len(rows) and desc.model_count == len(models)
+    for i, q in enumerate(rows):
+        assert list(qo[i].origin) == list(q["origin"]) and qo[i].material == q["material"]
+        assert list(qo[i].texture_u_range) == list(q["texture_u_range"])
+    rq[3].normal[0] += 0.5
+    assert lib.octpt_scene_from_reference(C.byref(ref), mo, to, qo, C.byref(desc)) == _lib.ERR_INVALID_ARG

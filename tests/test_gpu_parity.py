@@ -84,6 +84,7 @@ def assert_parity(gpu, ref, tag):
     assert st["segments"] == rst["segments"], tag
     assert st["esvo_steps"] == rst["esvo_steps"], tag
     assert st["sphere_tests"] + st["cuboid_tests"] == rst["prim_tests"], tag
+    assert st.get("block_tests", 0) == rst.get("block_tests", 0), tag  # block-value leaves (C23)
     assert st["shade_events"] == rst["shade_events"], tag
     assert np.all(np.isfinite(acc)), tag
     e = rel_err(acc, racc)

@@ -66,6 +66,10 @@ def test_bench_byte_counts():
     assert bench.extend_bytes(st) == 8 * 1000 + 20 * 10 + 28 * 5
     assert bench.extend_queue_bytes(st) == 40 * 7
     assert bench.shade_bytes(st) == 152 * 7 + 68 * 3 + 4 * 2 + 16 * 4
+    # the drain kernel's share (octpt_stats.drain) is not extend's
+    st["drain"] = {"esvo_steps": 100, "sphere_tests": 1, "cuboid_tests": 0, "segments": 2}
+    assert bench.extend_bytes(st) == 8 * 900 + 20 * 9 + 28 * 5
+    assert bench.extend_queue_bytes(st) == 40 * 5
 
 
 def test_bench_loads_committed_traffic():
