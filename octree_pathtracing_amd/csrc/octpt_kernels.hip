@@ -556,6 +556,10 @@ __device__ inline bool block_leaf_test(const DevScene &S, const TraceRay &r, con
     u = fabsf(u);
     v = fabsf(v);
     const uint32_t face = face_index(axis, neg ? 1.0f : -1.0f);  // the face entered faces against the ray
+    prim = (face << 27) | slot.x;
+    h.t = E.t_min * S.inv_octree_scale;
+    h.u = u;
+    h.v = v;
     if ((slot.y >> face) & 1u) {  // a face with alpha-0 texels: SingleBlockModel::intersect's texel
         const uint32_t mat = S.blk_mat[6u * slot.x + face];
         const DevMaterial &m = S.mats[mat];
@@ -570,10 +574,6 @@ __device__ inline bool block_leaf_test(const DevScene &S, const TraceRay &r, con
         }
         if (!(alpha > RAY_EPSILON)) return false;
     }
-    prim = (face << 27) | slot.x;
-    h.t = E.t_min * S.inv_octree_scale;
-    h.u = u;
-    h.v = v;
     return true;
 }
 
@@ -1578,6 +1578,12 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             bool cont = false;
             if (state != ST_FINISH) {
                 if (state == ST_HIT) commit_hit(S, ray, hprim, hh, cnt);
+#ifdef OCTPT_TRACE_PIXEL  // diagnostic build: one pixel's segments (megakernel)
+                if (pix == (uint32_t)OCTPT_TRACE_PIXEL)
+                    printf("GPU k=%u hit=%d prim=%08x t=%a u=%a v=%a o=(%a %a %a) d=(%a %a %a) col3=%a cur=%u rng=%08x\n", k,
+                           state == ST_HIT, hprim, hh.t, hh.u, hh.v, ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z,
+                           ray.col[3], ray.cur, ray.rng);
+#endif
                 cont = shade_segment<kNee>(S, R, ray, state == ST_HIT, cnt);
             }
             if (cont) {

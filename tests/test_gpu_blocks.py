@@ -9,7 +9,7 @@ render tolerances of tests/test_gpu_parity.py:
 - a tree built the way SectionOctantBuilder does (writer mask encoding, reversed post-order ids),
   uploaded through the reference-scene flattener octpt_scene_from_reference;
 - faces with alpha-0 texels (the traversal passes through them), sun sampling, preview, the batch
-  closest-hit query, the megakernel and the chunk-tail drain."""
+  closest-hit query and the megakernel (the chunk-tail drain: tests/test_gpu_drain.py)."""
 import ctypes as C
 
 import numpy as np
@@ -169,25 +169,6 @@ def test_block_megakernel_equals_wavefront(torch_cuda, renderer, name, res):
     b = gpu_render(torch_cuda, renderer, sc, cam, rs, megakernel=True)
     assert np.array_equal(a[1], b[1]) and rel_err(a[0], b[0]).max() <= 1e-5
     assert a[2]["esvo_steps"] == b[2]["esvo_steps"] and a[2]["block_tests"] == b[2]["block_tests"]
-
-
-def test_block_drain_identical(torch_cuda, renderer, monkeypatch):
-    """The chunk-tail drain on block-value scenes: results and statistics equal the drain switched off."""
-    from octree_pathtracing_amd.renderer import HipRenderer
-
-    sc, cam, rs = _config("C5s-small", (256, 144, 4), compact=True)
-    a = gpu_render(torch_cuda, renderer, sc, cam, rs)
-    monkeypatch.setenv("OCTPT_DRAIN_RAYS", "0")
-    r = HipRenderer(device=0)
-    monkeypatch.delenv("OCTPT_DRAIN_RAYS")
-    try:
-        b = gpu_render(torch_cuda, r, sc, cam, rs)
-    finally:
-        r.close()
-    assert a[2]["drain"]["segments"] > 0 and b[2]["drain"]["segments"] == 0
-    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32)) and np.array_equal(a[1], b[1])
-    for k in ("segments", "esvo_steps", "block_tests", "shade_events"):
-        assert a[2][k] == b[2][k], k
 
 
 def test_c5b_fullwidth_band(torch_cuda, renderer):

@@ -4,7 +4,7 @@ the wavefront's own per-segment code and record formats, so a render with the dr
 to one without it (OCTPT_DRAIN_RAYS=0): radiance, per-pixel segment counts and every statistic, on
 sphere, box, sun-sampling and branch-count scenes, and with a pool small enough that several chunks
 each end in a drain.  Block-model scenes (C5, blocks) keep the tail iterations; their cases check
-that the switch leaves them alone."""
+that the switch leaves them alone.  Block-value scenes (C23: C5b, blocks-b, C5s-small) drain."""
 import os
 
 import numpy as np
@@ -14,7 +14,8 @@ from tests.test_gpu_parity import gpu_render, renderer, torch_cuda  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 
-STATS = ("paths", "segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events", "texel_reads")
+STATS = ("paths", "segments", "esvo_steps", "sphere_tests", "cuboid_tests", "shade_events", "texel_reads",
+         "block_tests")
 
 
 def _renderer_with(env):
@@ -56,7 +57,9 @@ def _same(a, b):
 @pytest.mark.parametrize("name,res,variant,bc", [("C3", (480, 270, 4), None, 1), ("C2", (320, 180, 8), None, 1),
                                                  ("C4", (256, 144, 2), None, 1), ("C5", (256, 144, 2), None, 1),
                                                  ("blocks", None, None, 1), ("tiny", None, "hq", 1),
-                                                 ("C2", (160, 90, 4), "nee_importance", 1), ("tiny", None, None, 4)])
+                                                 ("C2", (160, 90, 4), "nee_importance", 1), ("tiny", None, None, 4),
+                                                 ("C5b", (256, 144, 2), None, 1), ("blocks-b", None, None, 1),
+                                                 ("C5s-small", (256, 144, 4), "fast", 1)])
 def test_drain_equals_wavefront(torch_cuda, renderer, no_drain, small_pool_drain, name, res, variant, bc):
     from octree_pathtracing_amd import scene as S
 
