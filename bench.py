@@ -190,6 +190,12 @@ def issued_probe(sc, cam, rs, dev_idx: int, ext_s: float):
                      "one render of the same step, divided by the timed library's mean extend launch time"}
 
 
+def scene_contents(sc) -> str:
+    if sc.blocks is not None:  # block-value leaves
+        return f"{len(sc.cells)} voxel cells as block-value leaves ({len(sc.blocks)} block kinds)"
+    return f"{len(sc.spheres)} spheres + {len(sc.cuboids)} cuboids"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -240,9 +246,9 @@ def main():
     from octree_pathtracing_amd.distributed import gather_frame
     from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
 
-    sc, cam, rs = S.make_config(args.config)
+    sc, cam, rs = S.make_config(args.config, build=not args.compact)
     if args.compact:
-        sc.build_octree(sc.octree.depth, compact=True)
+        sc.build_octree(sc._depth, compact=True)
     if args.spp:
         rs.spp = args.spp
     W, H = rs.width, rs.height
@@ -324,9 +330,9 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.config}: {len(sc.spheres)} spheres + {len(sc.cuboids)} cuboids, octree depth "
-                        f"{sc.octree.depth}{' (compacted)' if args.compact else ''}, {W}x{H}, {rs.spp} spp, "
-                        f"max_depth {rs.max_depth}, seed {rs.seed}",
+            "workload": f"{args.config}: {scene_contents(sc)}, octree depth {sc.octree.depth} "
+                        f"({sc.octree.octant_count} octants{', compacted' if args.compact else ''}), {W}x{H}, "
+                        f"{rs.spp} spp, max_depth {rs.max_depth}, seed {rs.seed}",
             "resolution": [W, H],
             "spp": rs.spp,
             "parallelism": (f"tiles{world}" + ("-gloo" if host_staged else "")) if world > 1 else "single",

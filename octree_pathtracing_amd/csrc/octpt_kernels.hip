@@ -822,6 +822,13 @@ __device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uin
 // +-1 % on C3 / C2 / C4, so only the block-model instance runs it (A/B: -DOCTPT_DFOLD=0 / 1 = all)
 #define OCTPT_DFOLD 3
 #endif
+// the block-value instance (C23): absent-sibling folds per step and the descend fold (A/B knobs)
+#ifndef OCTPT_FOLD_BLOCKS
+#define OCTPT_FOLD_BLOCKS 2
+#endif
+#ifndef OCTPT_DFOLD_BLOCKS
+#define OCTPT_DFOLD_BLOCKS 1
+#endif
 
 
 // leaf primitive list test [C1].  Leaf slot = (first list index, count), or (prim id, 1) for the
@@ -1000,7 +1007,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // descend-after-descend pairs (tools/esvo_trace.py).  That iteration is run here as an exact
     // replica (its own stop tests, t_corner, push and child choice, counted in E.iter); its slot
     // load depends on this step's, which the other waves of the SIMD hide.
-    if ((OCTPT_DFOLD != 3 || kPrims == kPrimsModels) && descend) {
+    if ((OCTPT_DFOLD != 3 || kPrims == kPrimsModels || (kPrims == kPrimsBlocks && OCTPT_DFOLD_BLOCKS)) && descend) {
         const uint32_t cidx2 = E.idx ^ E.mirror;
         const v3 tc2 = vsub(vmul(E.pos, E.t_coef), E.t_bias);
         const float tc2_max = tmin3(tc2);
@@ -1024,7 +1031,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // tests), so the wave does not pay a whole loop iteration for it.  44 % of C3's iterations are
     // such advances; folding the first of each run leaves 72 % of the iterations (tools/esvo_trace.py).
     // A fold that leaves the parent pops below, exactly as that iteration would.
-    constexpr int kFolds = kPrims == kPrimsModels ? OCTPT_FOLD_MODELS : OCTPT_FOLD;
+    constexpr int kFolds = kPrims == kPrimsModels ? OCTPT_FOLD_MODELS : kPrims == kPrimsBlocks ? OCTPT_FOLD_BLOCKS : OCTPT_FOLD;
 #pragma unroll
     for (int k = 0; k < kFolds; ++k) {  // kFolds folds at most per step
     const bool fold = !leaf_hit & !stopped & !pop & (((E.pmask >> (E.idx ^ E.mirror)) & 1u) == 0u) &
@@ -1895,7 +1902,7 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #define OCTPT_MDL_WAVES 6  // 95 -> 80 VGPRs, 36 B/lane spilled: C5 +5.4 %
 #endif
 #ifndef OCTPT_BLK_WAVES
-#define OCTPT_BLK_WAVES 7  // block-value leaves (C23)
+#define OCTPT_BLK_WAVES 6  // block-value leaves (C23); LDS holds depth-11 worlds (C5b, C5s) at 6 blocks per CU
 #endif
 #define OCTPT_EXTEND_WAVES_OF(k)                                                                              \
     ((k) == kPrimsSpheres ? OCTPT_SPH_WAVES                                                                   \
