@@ -895,8 +895,12 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
                      ctx->num_cu, ctx->S.depth, ctx->S.has_cuboids, ctx->S.has_models, pool);
     // shade maps waves to queue segments: a multiple of kSegs waves (kSegs / 4 blocks)
     const int seg_blocks = (int)(kSegs * 64u / kBlock);
-    const int shade_bpc = (int)std::min<uint32_t>(env_u32("OCTPT_SHADE_BPC", 4u), 8u);  // blocks per CU
-    const int grid_shade = (ctx->num_cu * shade_bpc + seg_blocks - 1) / seg_blocks * seg_blocks;
+    // blocks per CU: what the instance's registers allow (4 with regeneration, 5 without), or OCTPT_SHADE_BPC
+    const uint32_t shade_bpc_env = std::min<uint32_t>(env_u32("OCTPT_SHADE_BPC", 0u), 8u);
+    auto grid_shade_of = [&](bool regen) {
+        const int bpc = shade_bpc_env ? (int)shade_bpc_env : shade_blocks_per_cu(ctx->S, regen);
+        return (ctx->num_cu * bpc + seg_blocks - 1) / seg_blocks * seg_blocks;
+    };
     const WaveBuffers &B = ctx->wb;
     for (uint32_t c0 = 0, c1 = 0; c0 < R.spp_count; c0 = c1) {
         c1 = c0 + std::min(chunk_spp, R.spp_count - c0);
@@ -916,6 +920,8 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         const uint32_t chunk_items = (uint32_t)((uint64_t)Rc.spp_count * n_px);
         HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, kCtrlWords * sizeof(uint32_t), s));
         const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
+        const bool regen = n_seed < chunk_items;  // else the seed claimed every item of the chunk
+        const int grid_shade = grid_shade_of(regen);
         HIP_TRY(ctx, launch_wf_seed(ctx->C, Rc, B, n_seed, chunk_items, ctx->d_stats, s));
         for (uint32_t it = 0;; ++it) {
             if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
@@ -925,7 +931,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, grid_extend, ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
             if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
-            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, it == 0u, grid_shade, ctx->d_stats, s));
+            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, it == 0u, regen, grid_shade, ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 1, ev)) != OCTPT_OK) return st;
             // snapshot of the queue iteration `it` produced; the host checks the snapshot of
             // iteration it - kLookahead, so the GPU always has kLookahead iterations queued (an

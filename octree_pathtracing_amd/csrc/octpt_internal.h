@@ -208,9 +208,13 @@ hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuff
                           uint32_t chunk_items, unsigned long long *stats, hipStream_t stream);
 hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
                             unsigned long long *stats, hipStream_t stream);
-// first: the chunk's first shade (the seed's rays: path state rebuilt from item0)
+// first: the chunk's first shade (the seed's rays: path state rebuilt from item0); regen: the pool is
+// smaller than the chunk, finished paths regenerate their slots (the instance with regeneration)
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
-                           uint32_t chunk_items, bool first, int grid, unsigned long long *stats, hipStream_t stream);
+                           uint32_t chunk_items, bool first, bool regen, int grid, unsigned long long *stats,
+                           hipStream_t stream);
+// blocks per CU of the shade instance (registers bound it; shade uses no dynamic LDS)
+int shade_blocks_per_cu(const DevScene &S, bool regen);
 // the drain of a chunk's last queued rays (every chunk item claimed): one launch, paths finished in-lane
 hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuffers &B, uint32_t q, int grid,
                            unsigned long long *stats, hipStream_t stream);

@@ -2097,7 +2097,10 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
 #define OCTPT_SHADE_LDS_MATS 128
 #endif
 constexpr uint32_t kShadeLdsMats = OCTPT_SHADE_LDS_MATS;
-template <bool kNee, bool kLdsMats>
+// kRegen: finished lanes regenerate their slot with the next chunk items.  Only a pool smaller than
+// the chunk needs it (when the pool holds the chunk -- C3's frame, every 4K chunk -- the seed claimed
+// every item); the instance without it is 19 VGPRs leaner (96 instead of 115, 5 waves/SIMD instead of 4).
+template <bool kNee, bool kLdsMats, bool kRegen>
 __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items, uint32_t first,
                                                           unsigned long long *__restrict__ stats) {
@@ -2138,7 +2141,9 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
             finished = !append;
         }
         // regenerate: finished lanes take the next chunk items (path regeneration)
-        if (regen(C, R, B, slot, finished, chunk_items, cur, ps, cnt)) append = true;
+        if constexpr (kRegen) {
+            if (regen(C, R, B, slot, finished, chunk_items, cur, ps, cnt)) append = true;
+        }
         const uint32_t t = wave_ticket(B.ctrl + ctr_count(q ^ 1u, seg), append);
         if (append) store_ray(B, q ^ 1u, seg0 + t, slot, ps);
     }
@@ -2386,13 +2391,33 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
     return hipGetLastError();
 }
 
-hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
-                           uint32_t chunk_items, bool first, int grid, unsigned long long *stats, hipStream_t stream) {
+// the shade instance a scene and chunk launch (sun sampling, LDS material tables, regeneration)
+template <bool kNee, bool kLds>
+static const void *shade_instance_of(bool regen) {
+    return regen ? reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, true>)
+                 : reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, false>);
+}
+static const void *shade_instance(const DevScene &S, bool regen) {
     const bool lds = S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats;
-    auto kern = S.sun.sun_sampling ? (lds ? wf_shade_kernel<true, true> : wf_shade_kernel<true, false>)
-                                   : (lds ? wf_shade_kernel<false, true> : wf_shade_kernel<false, false>);
-    const uint32_t first_u = first ? 1u : 0u;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, stream, S, C, R, B, q, chunk_items, first_u, stats);
+    return S.sun.sun_sampling ? (lds ? shade_instance_of<true, true>(regen) : shade_instance_of<true, false>(regen))
+                              : (lds ? shade_instance_of<false, true>(regen) : shade_instance_of<false, false>(regen));
+}
+
+int shade_blocks_per_cu(const DevScene &S, bool regen) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, shade_instance(S, regen), kBlock, 0) != hipSuccess)
+        return 4;
+    return blocks > 0 ? blocks : 1;
+}
+
+hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
+                           uint32_t chunk_items, bool first, bool regen, int grid, unsigned long long *stats,
+                           hipStream_t stream) {
+    uint32_t first_u = first ? 1u : 0u;
+    void *args[] = {const_cast<DevScene *>(&S), const_cast<DevCamera *>(&C), const_cast<DevRender *>(&R),
+                    const_cast<WaveBuffers *>(&B), &q, &chunk_items, &first_u, &stats};
+    const hipError_t e = hipLaunchKernel(shade_instance(S, regen), dim3(grid), dim3(kBlock), args, 0, stream);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
