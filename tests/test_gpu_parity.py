@@ -287,43 +287,22 @@ def test_edge_cases(torch_cuda, renderer, case):
     assert_parity(gpu, ref, case)
 
 
-def test_c3_fullsize_band(torch_cuda, renderer):
-    """Headline scene at full 1920x1080: a 16-row band matches the oracle exactly (control flow)
-    and within tolerance (radiance); the whole frame is finite and non-negative."""
+@pytest.mark.parametrize("name,spp", [("C3", 2), ("C4", 1), ("C5", 1)])
+def test_fullframe_oracle(torch_cuda, renderer, name, spp):
+    """The benchmark configs at full size (C3 1920x1080, C4 / C5 3840x2160) against the oracle over the
+    WHOLE frame: per-pixel segment counts and the ESVO / primitive-test / shade totals exact, radiance
+    within the forward tolerance on every channel (the oracle takes a few seconds per frame on the
+    box's 16-thread CPU share)."""
     from octree_pathtracing_amd import scene as S
-    from oracle import cpu_ref
-
-    sc, cam, rs = S.make_config("C3")
-    rs.spp = 1
-    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs)
-    assert np.all(np.isfinite(acc)) and acc[..., :3].min() >= 0
-    assert st["paths"] == rs.width * rs.height
-    r0, r1 = 532, 548
-    racc, rsegs, _ = cpu_ref.render(sc, cam, rs.width, rs.height, 1, max_depth=5, seed=rs.seed, forward=True,
-                                    rows=(r0, r1))
-    assert np.array_equal(segs[r0:r1], rsegs[r0:r1])
-    assert rel_err(acc[r0:r1], racc[r0:r1]).max() <= REL_TOL_FORWARD
-
-
-@pytest.mark.parametrize("name", ["C4", "C5"])
-def test_4k_fullsize_band(torch_cuda, renderer, name):
-    """The two 4K configs at full 3840x2160, 1 spp: the whole frame is finite and non-negative and
-    a 16-row band through the middle of the frame matches the oracle exactly in per-pixel segment
-    counts and within the forward tolerance in radiance (as test_c3_fullsize_band)."""
-    from octree_pathtracing_amd import scene as S
-    from oracle import cpu_ref
 
     sc, cam, rs = S.make_config(name)
-    assert (rs.width, rs.height) == (3840, 2160)
-    rs.spp = 1
-    acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs)
-    assert np.all(np.isfinite(acc)) and acc[..., :3].min() >= 0
-    assert st["paths"] == rs.width * rs.height
-    r0, r1 = rs.height // 2 - 8, rs.height // 2 + 8
-    racc, rsegs, _ = cpu_ref.render(sc, cam, rs.width, rs.height, 1, max_depth=rs.max_depth, seed=rs.seed,
-                                    forward=True, rows=(r0, r1), threads=16)
-    assert np.array_equal(segs[r0:r1], rsegs[r0:r1])
-    assert rel_err(acc[r0:r1], racc[r0:r1]).max() <= REL_TOL_FORWARD
+    assert (rs.width, rs.height) == ((1920, 1080) if name == "C3" else (3840, 2160))
+    rs.spp = spp
+    gpu = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    assert gpu[2]["paths"] == rs.width * rs.height * spp
+    assert gpu[0][..., :3].min() >= 0
+    exact = assert_parity(gpu, oracle(sc, cam, rs, forward=True, threads=16), name)
+    assert exact > 0.999, f"{name}: only {exact:.4%} of channels bit-identical"
 
 
 def test_c3_fullframe_repeatable(torch_cuda, renderer):
