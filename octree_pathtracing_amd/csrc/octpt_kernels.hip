@@ -235,6 +235,9 @@ struct Counters {
 // load one, primitives, quads, alpha texels -- to Counters::ib; the product build compiles it out.
 #ifdef OCTPT_COUNT_ISSUED
 #define ISSUED(cnt, bytes) ((cnt).ib += (uint32_t)(bytes))
+// named apart, so that a profile of bench.py (whose issued-bytes probe renders through this build)
+// lists the counting kernel separately from the timed one
+#define wf_extend_kernel wf_issued_extend_kernel
 #else
 #define ISSUED(cnt, bytes) ((void)0)
 #endif
