@@ -946,7 +946,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const bool descend = (kind == 0x001u) & !stopped & (E.t_min <= tv_max);
     uint2 slot = make_uint2(0u, 0u);
     const uint32_t sidx = E.parent + __popc(E.pmask & ((1u << cidx) - 1u));
-    if (take_leaf || descend) {
+    if (take_leaf | descend) {
         slot = S.node_child[sidx];
         ISSUED(cnt, 8);
     }
@@ -995,7 +995,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // 1..depth-1 (stack slot = level - 1 >= 0; the oracle's level-0 entry stays zero, like the miss
     // below).  One guarded write, so that the selects below stay branch-free.
     const uint32_t slot_u = (__float_as_uint(E.scale_exp2) >> 23) - 128u + S.depth;
-    if (descend && tc_max < E.h) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
+    if (descend & (tc_max < E.h)) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
     E.h = descend ? tc_max : E.h;
     E.parent = descend ? slot.x : E.parent;  // (octant, its mask)
     E.pmask = descend ? slot.y : E.pmask;
@@ -1003,7 +1003,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     E.t_max = descend ? tv_max : E.t_max;
     E.t_min = descend ? E.t_min : tc_max;
     E.idx = descend ? step_mask : (E.idx ^ step_mask);
-    bool pop = !descend && (E.idx & step_mask) != 0u;
+    bool pop = !descend & ((E.idx & step_mask) != 0u);
 #if OCTPT_DFOLD
     // Descend fold: a descend whose chosen child is again an octant the ray enters is followed, in
     // the reference, by an iteration that only descends (:216-244); 26 % of C3's iterations are such
