@@ -1072,7 +1072,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const uint32_t scale_raw = 31u - (uint32_t)__clz(diff);
         // escaping the root is a miss (:281-283); its lane finishes the block on a clamped scale
         // and reports the miss at the end, so the pop stays one branch level
-        escaped = scale_raw >= OCTREE_MAX_SCALE;
+        const bool esc = scale_raw >= OCTREE_MAX_SCALE;
         const uint32_t scale = min(scale_raw, OCTREE_MAX_SCALE - 1u);
         E.scale_exp2 = __uint_as_float((scale - OCTREE_MAX_SCALE + 127u) << 23);
         // a pop rises above the level it advanced at (the step's own bit, 2^(s-23) in pos's
@@ -1089,9 +1089,14 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const uint32_t px = __float_as_uint(E.pos.x) & keep, py = __float_as_uint(E.pos.y) & keep,
                        pz = __float_as_uint(E.pos.z) & keep;
         E.pos = V(__uint_as_float(px), __uint_as_float(py), __uint_as_float(pz));
-        E.idx = ((px >> scale) & 1u) | (((py >> scale) & 1u) << 1) | (((pz >> scale) & 1u) << 2);
-        E.h = 0.0f;
+        E.idx = __builtin_amdgcn_ubfe(px, scale, 1u) | (__builtin_amdgcn_ubfe(py, scale, 1u) << 1) |
+                (__builtin_amdgcn_ubfe(pz, scale, 1u) << 2);
+        // h = 0 after a pop (:298); an escaped lane's h = -1 carries the escape out of the branch, where
+        // one compare turns it into a lane mask (a bool assigned in the branch became a VGPR 0/1 and
+        // cost a select and an OR at the merge).  The lane finishes here, so its h is never read.
+        E.h = esc ? -1.0f : 0.0f;
     }
+    escaped = pop & (E.h < 0.0f);
     return leaf_hit ? kStepHit : ((escaped | stopped) ? kStepMiss : kStepContinue);
 }
 
