@@ -4,7 +4,9 @@ Each seed draws a scene kind (spheres; spheres + cuboids; image-textured spheres
 transparent texels; voxel blocks with block models), an octree depth 2-10, primitive counts and sizes,
 emitters, a sun-sampling strategy (C18), the octree form (builder output, compacted C22, or the
 reference writer's mask encoding C21), a camera inside or outside the octree cube with a random field
-of view, max_depth and render seed.  The wavefront render must meet tests/test_gpu_parity.py's bar
+of view, max_depth and render seed.  Block seeds (kind 4) draw a block-value world (C23): the voxel world
+with block models as block leaves, or solid columns whose interior compacts into LOD leaves, with
+alpha-0 texels on some blocks' faces.  The wavefront render must meet tests/test_gpu_parity.py's bar
 against the oracle (bit-exact per-pixel segment counts and work totals, radiance within 1e-5
 relative) and the preview (C16) must be bit-exact.  Seeds are fixed, so a failure reproduces."""
 import numpy as np
@@ -16,17 +18,47 @@ from tests.test_gpu_parity import assert_parity, gpu_render, oracle, renderer, t
 pytestmark = pytest.mark.gpu
 
 SEEDS = list(range(1000, 1032))
+BLOCK_SEEDS = list(range(2000, 2016))
 
 
-def fuzz_scene(seed):
+def _block_world(S, sc, rng, seed, world):
+    """kind 4: the kind-3 voxel world as block-value leaves, or solid columns (C23)."""
+    if rng.random() < 0.5:
+        return S.voxels_to_blocks(sc)
+    side = int(min(world - 2, rng.integers(4, 40)))
+    h = rng.integers(1, max(2, min(int(world) - 3, 20)), (side, side))
+    col = [(x + 1, y, z + 1, 1 if y < h[x, z] - 1 else 2) for x in range(side) for z in range(side)
+           for y in range(int(h[x, z]))]
+    out = S.Scene(materials=sc.materials, textures=sc.textures)
+    mats = S.block_materials(out, seed)
+    names = list(S.BLOCK_TILES)
+    out.blocks = np.array([[mats[names[(b + f) % len(names)]] for f in range(6)] for b in range(3)], np.uint32)
+    out.block_model = np.full(3, 0xFFFFFFFF, np.uint32)
+    out.cells = np.array(col, np.uint32).reshape(-1, 4)
+    return out
+
+
+def _alpha_faces(S, sc, rng, seed):
+    """alpha-0 texels on some faces of some blocks (the traversal passes through them, C23)"""
+    mask = rng.random((16, 16)) < 0.4
+    sc.textures.append(S.Texture.image(S.alpha_tile(seed, 77, (200, 220, 235), 12, mask)))
+    sc.materials.append(S.Material(texture_index=len(sc.textures) - 1))
+    m = len(sc.materials) - 1
+    full = np.asarray(sc.block_model) == 0xFFFFFFFF
+    for b in np.flatnonzero(full):
+        if rng.random() < 0.5:
+            sc.blocks[b, rng.random(6) < 0.5] = m
+
+
+def fuzz_scene(seed, kind=None):
     from octree_pathtracing_amd import scene as S
 
     rng = np.random.default_rng(seed)
-    kind = seed % 4
+    kind = seed % 4 if kind is None else kind
     depth = int(rng.integers(2, 11))
     world = float(1 << depth)
     sc = S.Scene()
-    if kind == 3:  # voxel blocks + block models (C19) on a random height field
+    if kind >= 3:  # voxel blocks + block models (C19) on a random height field
         side = int(min(world - 2, rng.integers(4, 40)))
         xz = np.stack(np.meshgrid(np.arange(side), np.arange(side), indexing="ij"), -1).reshape(-1, 2) + 1
         h = rng.integers(1, max(2, min(int(world) - 3, 12)), len(xz))
@@ -36,6 +68,10 @@ def fuzz_scene(seed):
         on = pos[rng.random(len(pos)) < 0.3] + np.array([0, 1, 0])
         on = on[on[:, 1] < world - 1]
         S.place_models(sc, seed, ids_m, on)
+        if kind == 4:
+            sc = _block_world(S, sc, rng, seed, world)
+            if rng.random() < 0.5:
+                _alpha_faces(S, sc, rng, seed)
     else:
         ids = S.textured_materials(sc, seed) if kind == 2 else S.primitive_materials(sc)
         n_s = int(rng.integers(1, 300))
@@ -68,6 +104,13 @@ def fuzz_scene(seed):
         eye = rng.uniform(-0.4 * world, 1.4 * world, 3)
         eye[int(rng.integers(0, 3))] = rng.choice([-0.3 * world, 1.3 * world])
     target = rng.uniform(0.25 * world, 0.75 * world, 3)
+    if kind == 4:  # block worlds sit in a corner of the cube: aim at them, from up to 3 extents away
+        cells = np.asarray(sc.cells, np.float64)[:, :3]
+        lo, hi = cells.min(0), cells.max(0) + 1.0
+        target = rng.uniform(lo, hi)
+        ext = float((hi - lo).max())
+        eye = target + rng.normal(size=3) * rng.uniform(0.3, 3.0) * ext
+        eye[1] = abs(eye[1] - target[1]) + target[1] if rng.random() < 0.8 else eye[1]  # mostly from above
     fov = float(np.float32(rng.uniform(30.0, 100.0)) * np.float32(np.pi / 180.0))
     cam = S.Camera.look_at(tuple(map(float, eye)), tuple(map(float, target)), fov=fov)
     rs = S.RenderSettings(int(rng.integers(8, 96)), int(rng.integers(8, 64)), int(rng.integers(1, 4)),
@@ -81,9 +124,15 @@ def test_fuzz_render_parity(torch_cuda, renderer, seed):
     assert_parity(gpu_render(torch_cuda, renderer, sc, cam, rs), oracle(sc, cam, rs, forward=True), tag)
 
 
-@pytest.mark.parametrize("seed", SEEDS[::3])
+@pytest.mark.parametrize("seed", BLOCK_SEEDS)
+def test_fuzz_block_render_parity(torch_cuda, renderer, seed):
+    sc, cam, rs, tag = fuzz_scene(seed, kind=4)
+    assert_parity(gpu_render(torch_cuda, renderer, sc, cam, rs), oracle(sc, cam, rs, forward=True), tag)
+
+
+@pytest.mark.parametrize("seed", SEEDS[::3] + BLOCK_SEEDS[::4])
 def test_fuzz_preview_parity(torch_cuda, renderer, seed):
-    sc, cam, rs, tag = fuzz_scene(seed)
+    sc, cam, rs, tag = fuzz_scene(seed, kind=4 if seed >= 2000 else None)
     acc, segs, st = gpu_render(torch_cuda, renderer, sc, cam, rs, preview=True)
     racc, rsegs, rst = oracle(sc, cam, rs, preview=True)
     assert np.array_equal(segs, rsegs), tag
