@@ -1958,7 +1958,6 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t c_next = 0u, c_end = 0u, claim_v = 0u;
     uint32_t thr = refill ? refill : OCTPT_THR_LONG;  // idle lanes that trigger a refill (wave-uniform)
-    uint32_t lane_rays = 0u;                // rays this lane started (adaptive threshold)
     if (lane == 0u)
         claim_v = __hip_atomic_fetch_add(B.ctrl + ctr_head(q, seg), kClaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     do {
@@ -1994,7 +1993,6 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk);
                     active = true;
-                    lane_rays++;
                 }
             }
             const uint32_t took = min((uint32_t)__popcll(im), avail);
@@ -2003,7 +2001,9 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
             if (refill == 0u) {
                 // adaptive threshold: when most lanes' rays so far averaged fewer
                 // than kShortRaySteps ESVO steps, the wave refills 32 at a time, else 16
-                const bool short_rays = cnt.steps < kShortRaySteps * lane_rays;
+                // (a lane's rays counted as the wave's average, segs_w / 64: no per-lane counter, which
+                // the block instance spilled to scratch at every refill)
+                const bool short_rays = cnt.steps * 64u < kShortRaySteps * segs_w;
                 thr = __popcll(__ballot(short_rays)) > 32 ? OCTPT_THR_SHORT : OCTPT_THR_LONG;
             }
         }
