@@ -1971,7 +1971,10 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                                        : c_next;
                 if (c_next >= c_end) {
                     // segment drained: lane j checks segment j, the wave moves on and claims there
-                    const uint32_t j = lane;
+                    // (j passed through an empty asm: the two per-lane counter addresses are formed
+                    // here, not hoisted out of the loop into registers that the loop then spills)
+                    uint32_t j = lane;
+                    if constexpr (kPrims != kPrimsSpheres) asm volatile("" : "+v"(j));
                     const uint64_t m = __ballot(relaxed_load(B.ctrl + ctr_head(q, j)) < B.ctrl[ctr_count(q, j)]);
                     rays_left = m != 0ull;
                     if (rays_left) {
@@ -2019,11 +2022,16 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 PrimHit h;
                 const int rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
                 if (rs != kStepContinue) {
+                    // the record's address is formed here from pos (through an empty asm), not kept
+                    // from the refill in two more registers that the loop would spill (not in the
+                    // sphere instance, whose allocation is better off as it is: C3 -1 % with it)
+                    uint32_t p = pos;
+                    if constexpr (kPrims != kPrimsSpheres) asm volatile("" : "+v"(p));
                     if constexpr (kPrims == kPrimsBlocks) {  // (face << 27 | block or the quad, t) + (u, v) (C23)
-                        B.hit[pos] = rs == kStepHit ? make_uint2(prim, __float_as_uint(h.t)) : make_uint2(kPrimNone, 0u);
-                        if (rs == kStepHit) B.huv[pos] = make_float2(h.u, h.v);
+                        B.hit[p] = rs == kStepHit ? make_uint2(prim, __float_as_uint(h.t)) : make_uint2(kPrimNone, 0u);
+                        if (rs == kStepHit) B.huv[p] = make_float2(h.u, h.v);
                     } else {
-                        B.hit[pos] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                        B.hit[p] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
                     }
                     cnt.steps += E.iter;
                     active = false;
