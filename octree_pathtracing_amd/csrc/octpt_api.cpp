@@ -112,6 +112,7 @@ struct octpt_ctx {
     hipEvent_t count_ev[kLookahead + 1] = {};
     uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
     uint32_t drain_rays = kDefaultDrainRays;  // queue length at which the drain takes over (OCTPT_DRAIN_RAYS, 0 = off)
+    bool drain_models = false;                // the drain in block-model scenes too (OCTPT_DRAIN_MODELS=1, A/B)
     uint64_t chunk_cap = kDefaultChunkPaths;  // (pixel, sample) items per chunk (OCTPT_CHUNK)
     // one asynchronous frame may be in flight; device-touching calls join it first
     octpt_frame *inflight = nullptr;
@@ -957,7 +958,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
                 // tail of near-empty iterations.  Not in the extend timer (rocprof reports it as
                 // wf_drain_kernel); its statistics (<= 4096 paths) stay in the totals.
                 // (not for block-model scenes: their tails are transparent-texel chains, C5 -1 %)
-                if (queued <= ctx->drain_rays && !ctx->S.has_models) {
+                if (queued <= ctx->drain_rays && (!ctx->S.has_models || ctx->drain_models)) {
                     bool exhausted = true;
                     for (uint32_t k = 0; k < kSegs && exhausted; ++k) {
                         const uint32_t lo = (uint32_t)(((uint64_t)k * chunk_items) / kSegs);
@@ -1212,6 +1213,7 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     // OCTPT_DRAIN_RAYS=n: the drain's queue threshold; 0 turns the drain off (A/B)
     const char *drain_env = std::getenv("OCTPT_DRAIN_RAYS");
     if (drain_env && *drain_env) ctx->drain_rays = (uint32_t)std::strtoul(drain_env, nullptr, 10);
+    ctx->drain_models = env_u32("OCTPT_DRAIN_MODELS", 0u) != 0u;
     ctx->mem_limit = (size_t)env_u32("OCTPT_DEVICE_MEM_LIMIT", 0u) << 20;  // MiB, test hook (ensure_wave)
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
