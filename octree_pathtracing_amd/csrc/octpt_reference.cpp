@@ -30,6 +30,7 @@ extern "C" octpt_status octpt_scene_from_reference(const octpt_reference_scene *
     if (ref->material_count && (!ref->materials || !materials_out || !textures_out)) return OCTPT_ERR_INVALID_ARG;
     if (ref->quad_count && (!ref->quads || !quads_out)) return OCTPT_ERR_INVALID_ARG;
     if (ref->model_count && !ref->models) return OCTPT_ERR_INVALID_ARG;
+    if (ref->block_count && !ref->blocks) return OCTPT_ERR_INVALID_ARG;
     // Box<[Material]> -> material i with its own texture i (gpu_renderer.rs:221-307)
     for (uint32_t m = 0; m < ref->material_count; ++m) {
         const octpt_reference_material &x = ref->materials[m];

@@ -202,6 +202,8 @@ def test_scene_from_reference_fills_desc():
     blocks[0].face_material[2] = n
     ref.blocks = C.cast(blocks, C.c_void_p)
     assert lib.octpt_scene_from_reference(C.byref(ref), mo, to, qo, C.byref(desc)) == _lib.ERR_INVALID_ARG
+    ref.blocks = None  # a block count without its table
+    assert lib.octpt_scene_from_reference(C.byref(ref), mo, to, qo, C.byref(desc)) == _lib.ERR_INVALID_ARG
 
 
 def test_scene_from_reference_quads():
