@@ -15,6 +15,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "../../include/octpt.h"
@@ -1876,11 +1877,11 @@ octpt_status octpt_build_block_octree(const uint32_t *cells, uint32_t n, uint32_
         std::sort(sorted.begin(), sorted.end());
         for (size_t k = 1; k < sorted.size(); ++k)
             if (sorted[k].first == sorted[k - 1].first) return OCTPT_ERR_INVALID_ARG;  // two blocks in one cell
-        octpt_octree *t = new octpt_octree();
+        std::unique_ptr<octpt_octree> t(new octpt_octree());
         t->depth = depth;
-        BlockBuilder b{t, sorted, depth, (flags & OCTPT_BUILD_COMPACT) != 0};
+        BlockBuilder b{t.get(), sorted, depth, (flags & OCTPT_BUILD_COMPACT) != 0};
         t->root = b.node(0, 0, sorted.size()).v;
-        *out = t;
+        *out = t.release();
         return OCTPT_OK;
     } catch (const std::bad_alloc &) {
         return OCTPT_ERR_OOM;
