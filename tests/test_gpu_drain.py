@@ -75,3 +75,25 @@ def test_drain_equals_wavefront(torch_cuda, renderer, no_drain, small_pool_drain
     _same(a, b)
     c = gpu_render(torch_cuda, small_pool_drain, sc, cam, rs, branch_count=bc)
     _same(a, c)
+
+
+@pytest.fixture(scope="module")
+def drain_models(torch_cuda):
+    r = _renderer_with({"OCTPT_DRAIN_MODELS": "1", "OCTPT_POOL": "65536", "OCTPT_CHUNK": "200000"})
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("name,res", [("C5", (256, 144, 2)), ("blocks", None)])
+def test_drain_in_block_model_scenes(torch_cuda, renderer, drain_models, name, res):
+    """OCTPT_DRAIN_MODELS=1 (the A/B knob): block-model scenes drained too, with several
+    chunks, render bit-identically; the drain ran (its share is in the statistics' drain row)."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config(name)
+    if res:
+        rs.width, rs.height, rs.spp = res
+    a = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    b = gpu_render(torch_cuda, drain_models, sc, cam, rs)
+    _same(a, b)
+    assert b[2]["drain"]["segments"] > 0
