@@ -822,8 +822,14 @@ __device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uin
 #endif
 #ifndef OCTPT_DFOLD
 // descend fold in esvo_step, per instance: measured +4 % extend on C5 (block models, depth 11),
-// +-1 % on C3 / C2 / C4, so only the block-model instance runs it (A/B: -DOCTPT_DFOLD=0 / 1 = all)
+// +-1 % on C3 / C2 / C4 in round 2, so 3 = the block-model instance, plus the block-value and sphere
+// instances by their own knobs below (A/B: -DOCTPT_DFOLD=0 / 1 = all)
 #define OCTPT_DFOLD 3
+#endif
+// the sphere instance's descend fold (round 3, after the lane-mask and spill work: C3 extend -1.4..-2.1 %,
+// C2 -1 %; the box instance stays without it, C4 +0.4..+0.8 %)
+#ifndef OCTPT_DFOLD_SPHERES
+#define OCTPT_DFOLD_SPHERES 1
 #endif
 // the block-value instance (C23): absent-sibling folds per step and the descend fold (A/B knobs)
 #ifndef OCTPT_FOLD_BLOCKS
@@ -1010,7 +1016,8 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // descend-after-descend pairs (tools/esvo_trace.py).  That iteration is run here as an exact
     // replica (its own stop tests, t_corner, push and child choice, counted in E.iter); its slot
     // load depends on this step's, which the other waves of the SIMD hide.
-    if ((OCTPT_DFOLD != 3 || kPrims == kPrimsModels || (kPrims == kPrimsBlocks && OCTPT_DFOLD_BLOCKS)) && descend) {
+    if ((OCTPT_DFOLD != 3 || kPrims == kPrimsModels || (kPrims == kPrimsBlocks && OCTPT_DFOLD_BLOCKS) ||
+         (kPrims == kPrimsSpheres && OCTPT_DFOLD_SPHERES)) && descend) {
         const uint32_t cidx2 = E.idx ^ E.mirror;
         const v3 tc2 = vsub(vmul(E.pos, E.t_coef), E.t_bias);
         const float tc2_max = tmin3(tc2);
