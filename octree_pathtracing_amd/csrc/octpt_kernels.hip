@@ -1951,6 +1951,8 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
     // the wave starts on its home segment (seg, seg_n rays: wave-uniform)
     uint32_t seg = __builtin_amdgcn_readfirstlane(((blockIdx.x * kBlock + threadIdx.x) >> 6) % kSegs);
     uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
+    // (the block-model instance holds seg_n in an SGPR: in a VGPR it was spilled, C5 extend -1 %)
+    if constexpr (kPrims == kPrimsModels) seg_n = __builtin_amdgcn_readfirstlane(seg_n);
     bool rays_left = true;  // wave-uniform: some segment may still hold unclaimed rays
     uint32_t segs_w = 0u;   // segments started by this wave
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -1987,6 +1989,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                     if (rays_left) {
                         seg = __builtin_amdgcn_readfirstlane(first_from(m, seg));
                         seg_n = B.ctrl[ctr_count(q, seg)];
+                        if constexpr (kPrims == kPrimsModels) seg_n = __builtin_amdgcn_readfirstlane(seg_n);
                     }
                 }
                 if (rays_left && lane == 0u)
