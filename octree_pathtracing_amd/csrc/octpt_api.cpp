@@ -1337,7 +1337,6 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.leaf_prims = d_prims;
         S.root = base[d->root];  // traversal "parent" values are child-array bases
         S.root_mask = masks[d->root];
-        S.node0_mask = masks[0];  // base[0] == 0: a zeroed stack entry reads octant 0
         S.n_octants = d->octant_count;
         st = upload_tables(ctx, d, true, S);
         if (st != OCTPT_OK) return st;
@@ -1407,7 +1406,6 @@ octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *d,
         S.cub_mat = out.cub_mat;
         S.root = 0u;
         S.root_mask = root_mask;
-        S.node0_mask = root_mask;
         S.n_octants = t.n_octants;
         st = upload_tables(ctx, d, false, S);
         if (st != OCTPT_OK) return st;

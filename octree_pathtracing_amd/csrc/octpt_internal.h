@@ -85,7 +85,7 @@ struct DevScene {
     // (first leaf prim, prim count)
     const uint2 *node_child;
     const float4 *leaf_sph;         // parallel to node_child: the sphere of a single-sphere leaf slot
-    uint32_t root, root_mask, node0_mask, depth, n_octants;  // root = the root octant's base
+    uint32_t root, root_mask, depth, n_octants;  // root = the root octant's base
     uint32_t has_cuboids;
     float octree_scale;             // 2^-depth
     float inv_octree_scale;         // 2^depth (x / 2^-depth == x * 2^depth exactly)

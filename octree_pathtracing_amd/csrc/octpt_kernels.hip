@@ -781,9 +781,6 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (upper.y > E.t_min) { E.idx ^= 2u; E.pos.y = 1.5f; }
     if (upper.z > E.t_min) { E.idx ^= 4u; E.pos.z = 1.5f; }
     E.iter = 0u;
-#ifdef OCTPT_ZERO_STACK  // diagnostic: the oracle's zeroed stack (octant 0, t 0) instead of stale entries
-    for (uint32_t l = 0; l + 1u < S.depth; ++l) stk_write(stk, l, 0u, 0.0f, S.node0_mask);
-#endif
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
@@ -1600,12 +1597,6 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
             bool cont = false;
             if (state != ST_FINISH) {
                 if (state == ST_HIT) commit_hit(S, ray, hprim, hh, cnt);
-#ifdef OCTPT_TRACE_PIXEL  // diagnostic build: one pixel's segments (megakernel)
-                if (pix == (uint32_t)OCTPT_TRACE_PIXEL)
-                    printf("GPU k=%u hit=%d prim=%08x t=%a u=%a v=%a o=(%a %a %a) d=(%a %a %a) col3=%a cur=%u rng=%08x\n", k,
-                           state == ST_HIT, hprim, hh.t, hh.u, hh.v, ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z,
-                           ray.col[3], ray.cur, ray.rng);
-#endif
                 cont = shade_segment<kNee>(S, R, ray, state == ST_HIT, cnt);
             }
             if (cont) {

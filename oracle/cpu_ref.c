@@ -18,9 +18,6 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
-#ifdef REF_TRACE_PIXEL
-#include <stdio.h>
-#endif
 
 /* ------------------------------------------------------------------------- */
 /* constants                                                                  */
@@ -764,20 +761,10 @@ size_t ref_esvo_trace_len(void) { return g_trace_n; }
 static int esvo(ctx_t *c, const ray_t *ray, float max_dst_w, uint32_t *hit_prim, prim_hit *hit, uint32_t *steps_out) {
     const ref_scene *s = c->s;
     float octree_scale = c->octree_scale;
-#ifdef REF_STALE_STACK /* diagnostic: the stack keeps the previous ray's entries (the kernels' LDS stack) */
-    static __thread uint32_t st_node[OCTREE_MAX_SCALE + 1];
-    static __thread float st_t[OCTREE_MAX_SCALE + 1];
-    static __thread uint32_t st_seed = 0x9E3779B9u;
-    for (int k = 0; k <= OCTREE_MAX_SCALE; k++) { /* scramble what a stale read would see */
-        st_seed = st_seed * 747796405u + 2891336453u;
-        if (st_seed & 0x80000000u) { st_node[k] = st_seed % (s->n_octants ? s->n_octants : 1); st_t[k] = (float)(st_seed & 0xFFF) * 1e-4f; }
-    }
-#else
     uint32_t st_node[OCTREE_MAX_SCALE + 1];
     float st_t[OCTREE_MAX_SCALE + 1];
     memset(st_node, 0, sizeof st_node);
     memset(st_t, 0, sizeof st_t);
-#endif
     uint32_t steps = 0;
     v3 ro = vscale(ray->o, octree_scale);        /* :71 */
     v3 rd = ray->d;                               /* :73 */
@@ -1280,25 +1267,12 @@ static int do_transmission(ctx_t *c, const ray_t *ray, ray_t *next, float cum[4]
     return hit;
 }
 
-#ifdef REF_TRACE_PIXEL
-static __thread int g_trace_on;
-#endif
 static int path_trace(ctx_t *c, ray_t *ray, int first, uint32_t *rng, fwd_t *fw, uint32_t *segs) { /* :15-135 */
     int hit = 0;
     const ref_scene *s = c->s;
     for (;;) {
         if (c->path_segs >= MAX_PATH_SEGMENTS) break; /* [C15] */
-#ifdef REF_TRACE_PIXEL
-        ray_t before = *ray;
-        int hh = next_intersection(c, ray, segs);
-        if (g_trace_on)
-            fprintf(stderr, "REF hit=%d t=%a u=%a v=%a o=(%a %a %a) d=(%a %a %a) col3=%a cur=%u rng=%08x (from o=(%a %a %a))\n", hh,
-                    ray->t, ray->u, ray->v, ray->o.x, ray->o.y, ray->o.z, ray->d.x, ray->d.y, ray->d.z, ray->col[3],
-                    ray->cur_mat, *rng, before.o.x, before.o.y, before.o.z);
-        if (!hh) {
-#else
         if (!next_intersection(c, ray, segs)) {
-#endif
             if (ray->depth == 0) get_sky_color_interp(&c->sun, ray);
             else if (ray->specular) get_sky_color(&c->sun, ray, 1);
             else get_sky_color_diffuse_sun(&c->sun, ray, c->sun.diffuse_sun);
@@ -1461,10 +1435,6 @@ static void render_rows(job_t *j, ctx_t *c) {
                 c->st.paths++;
                 c->path_segs = 0;
                 float col[3];
-#ifdef REF_TRACE_PIXEL
-                g_trace_on = pix == (uint32_t)REF_TRACE_PIXEL;
-                if (g_trace_on) fprintf(stderr, "REF sample %u\n", spp);
-#endif
                 if (c->forward) {
                     fwd_t fw = {{1.0f, 1.0f, 1.0f}, {0.0f, 0.0f, 0.0f}};
                     path_trace(c, &ray, 1, &rng, &fw, &segs);
