@@ -96,6 +96,7 @@ struct octpt_ctx {
     BuildScratch build_scratch;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
     int extend_bpc_cache[kMaxDepth + 1][4] = {};  // [depth][kPrims]
+    int shade_bpc_cache[2][2][2] = {};            // [sun sampling][LDS tables][regeneration]
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
     size_t pool = 0, color_cap = 0, nee_pool = 0;  // nee_pool: slots of the sun-sampling planes (wb.pd)
@@ -900,7 +901,11 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     // blocks per CU: what the instance's registers allow (4 with regeneration, 5 without), or OCTPT_SHADE_BPC
     const uint32_t shade_bpc_env = std::min<uint32_t>(env_u32("OCTPT_SHADE_BPC", 0u), 8u);
     auto grid_shade_of = [&](bool regen) {
-        const int bpc = shade_bpc_env ? (int)shade_bpc_env : shade_blocks_per_cu(ctx->S, regen);
+        int &cached = ctx->shade_bpc_cache[ctx->S.sun.sun_sampling ? 1 : 0]
+                                          [shade_lds_tables(ctx->S) ? 1 : 0]
+                                          [regen ? 1 : 0];
+        if (cached == 0) cached = shade_blocks_per_cu(ctx->S, regen);
+        const int bpc = shade_bpc_env ? (int)shade_bpc_env : cached;
         return (ctx->num_cu * bpc + seg_blocks - 1) / seg_blocks * seg_blocks;
     };
     const WaveBuffers &B = ctx->wb;

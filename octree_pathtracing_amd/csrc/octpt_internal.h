@@ -215,6 +215,8 @@ hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRende
                            hipStream_t stream);
 // blocks per CU of the shade instance (registers bound it; shade uses no dynamic LDS)
 int shade_blocks_per_cu(const DevScene &S, bool regen);
+// whether the scene's shade instance copies the material / texture tables into LDS
+bool shade_lds_tables(const DevScene &S);
 // the drain of a chunk's last queued rays (every chunk item claimed): one launch, paths finished in-lane
 hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuffers &B, uint32_t q, int grid,
                            unsigned long long *stats, hipStream_t stream);

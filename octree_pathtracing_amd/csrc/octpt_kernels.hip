@@ -2414,8 +2414,9 @@ static const void *shade_instance_of(bool regen) {
     return regen ? reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, true>)
                  : reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, false>);
 }
+bool shade_lds_tables(const DevScene &S) { return S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats; }
 static const void *shade_instance(const DevScene &S, bool regen) {
-    const bool lds = S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats;
+    const bool lds = shade_lds_tables(S);
     return S.sun.sun_sampling ? (lds ? shade_instance_of<true, true>(regen) : shade_instance_of<true, false>(regen))
                               : (lds ? shade_instance_of<false, true>(regen) : shade_instance_of<false, false>(regen));
 }
