@@ -908,6 +908,11 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         const int bpc = shade_bpc_env ? (int)shade_bpc_env : cached;
         return (ctx->num_cu * bpc + seg_blocks - 1) / seg_blocks * seg_blocks;
     };
+    {
+        float none;
+        std::memcpy(&none, &kPrimNone, sizeof none);
+        ctx->wb.eye = make_float4(ctx->C.eye[0], ctx->C.eye[1], ctx->C.eye[2], none);
+    }
     const WaveBuffers &B = ctx->wb;
     for (uint32_t c0 = 0, c1 = 0; c0 < R.spp_count; c0 = c1) {
         c1 = c0 + std::min(chunk_spp, R.spp_count - c0);

@@ -176,6 +176,9 @@ struct WaveBuffers {
     uint32_t pool;
     uint32_t *ctrl;    // kCtrlWords sharded counters (see above)
     uint32_t seg_cap;  // positions per queue segment (multiple of 64)
+    // (camera eye.xyz, kPrimNone): the first half of every ray record the seed writes, which the
+    // chunk's first shade takes from here instead of re-reading it
+    float4 eye;
 };
 
 // per-launch statistics, accumulated with one atomic per wave

@@ -2064,7 +2064,7 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
         float4 a, b;
         uint2 c;
         pack_path(s0, item, a, b, c);
-        unpack_path(a, b, c, r0, r1, ps, item);
+        unpack_path(a, b, c, B.eye, r1, ps, item);  // a camera ray's ray0 is (eye, kPrimNone): not re-read
     } else {
         load_path(B, slot, r0, r1, ps, item);
     }
@@ -2153,7 +2153,8 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
         bool append = false, finished = false;
         PathState ps;
         if (valid) {
-            const float4 r0 = B.ray0[q][i], r1 = B.ray1[q][i];
+            const float4 r1 = B.ray1[q][i];
+            const float4 r0 = first ? B.eye : B.ray0[q][i];  // (the chunk's first shade: the seed's camera rays)
             append = shade_lane<kNee>(S, C, R, B, first != 0u, r0, r1, B.hit + i, B.huv + i, ps, slot, item, cnt);
             finished = !append;
         }
