@@ -546,6 +546,7 @@ octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_
     // the block instance (has_blocks)
     S.has_models = (has_models && !d->blocks) ? 1u : 0u;
     S.has_blocks = d->blocks ? 1u : 0u;
+    S.n_blocks = d->blocks ? d->block_count : 0u;
     S.blk_mat = d_blk_mat;
     S.blk_model = d_blk_model;
     S.mats = d_mats;

@@ -101,7 +101,7 @@ struct DevScene {
     uint32_t has_models;
     // block-value leaves (C23): a leaf slot is (block id, kBlock* flags); blk_mat = 6 face materials per
     // block, blk_model = its model (OCTPT_MODEL_NONE: the block fills its cell)
-    uint32_t has_blocks;
+    uint32_t has_blocks, n_blocks;
     const uint32_t *blk_mat;
     const uint32_t *blk_model;
     const DevMaterial *mats;

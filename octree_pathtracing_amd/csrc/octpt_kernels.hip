@@ -2114,6 +2114,11 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
 #define OCTPT_SHADE_LDS_MATS 128
 #endif
 constexpr uint32_t kShadeLdsMats = OCTPT_SHADE_LDS_MATS;
+// ... and at most this many blocks (C23) their face-material table
+#ifndef OCTPT_SHADE_LDS_BLOCKS
+#define OCTPT_SHADE_LDS_BLOCKS 128
+#endif
+constexpr uint32_t kShadeLdsBlocks = OCTPT_SHADE_LDS_BLOCKS;
 // kRegen: finished lanes regenerate their slot with the next chunk items.  Only a pool smaller than
 // the chunk needs it (when the pool holds the chunk -- C3's frame, every 4K chunk -- the seed claimed
 // every item); the instance without it is 19 VGPRs leaner (96 instead of 115, 5 waves/SIMD instead of 4).
@@ -2125,16 +2130,23 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
     __shared__ DevMaterial smats[kT];
     __shared__ DevTexture stexs[kT];
     __shared__ float slut[kLdsMats ? 256 : 1];
+    __shared__ uint32_t sblk[kLdsMats ? 6u * kShadeLdsBlocks : 1];
     DevScene S = Sg;
     if constexpr (kLdsMats) {
         for (uint32_t m = threadIdx.x; m < Sg.n_mats; m += kBlock) smats[m] = Sg.mats[m];
         for (uint32_t t = threadIdx.x; t < Sg.n_texs; t += kBlock) stexs[t] = Sg.texs[t];
         static_assert(kBlock == 256u, "one LUT entry per thread");
         slut[threadIdx.x] = Sg.lut_float[threadIdx.x];
+        // block-value scenes: the block -> face material table too (C5b: 10 blocks), so that a block
+        // hit's material is an LDS read, not a dependent global load before the texel's
+        const bool lds_blk = Sg.has_blocks && Sg.n_blocks <= kShadeLdsBlocks;
+        if (lds_blk)
+            for (uint32_t k = threadIdx.x; k < 6u * Sg.n_blocks; k += kBlock) sblk[k] = Sg.blk_mat[k];
         __syncthreads();
         S.mats = smats;
         S.texs = stexs;
         S.lut_float = slut;
+        if (lds_blk) S.blk_mat = sblk;
     }
     // wave w shades segment w % kSegs of queue q (grid: a multiple of kSegs waves) and appends
     // the continuing / regenerated rays to the same segment of queue q ^ 1
