@@ -79,6 +79,9 @@ struct octpt_ctx {
     std::vector<uint2> h_subs;
     uint2 *d_subs = nullptr;
     size_t subs_cap = 0;
+    // beam starts of the camera rays, one per 8x8 tile (beam_kernel), grow-only
+    float *d_beam = nullptr;
+    size_t beam_cap = 0;
     uint32_t launch_seq = 0;
     unsigned long long *d_stats = nullptr;
     uint8_t *d_lut_byte = nullptr;
@@ -113,6 +116,7 @@ struct octpt_ctx {
     uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
     hipEvent_t count_ev[kLookahead + 1] = {};
     uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
+    bool beam = true;  // camera rays start at their tile's beam (OCTPT_BEAM=0: off)
     uint32_t drain_rays = kDefaultDrainRays;  // queue length at which the drain takes over (OCTPT_DRAIN_RAYS, 0 = off)
     bool drain_models = false;                // the drain in block-model scenes too (OCTPT_DRAIN_MODELS=1, A/B)
     uint64_t chunk_cap = kDefaultChunkPaths;  // (pixel, sample) items per chunk (OCTPT_CHUNK)
@@ -626,6 +630,8 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     R.total_items = R.shard_tiles * 64u;
     R.dim = (float)std::max(p->width, p->height);
     R.subs = nullptr;
+    R.beam = nullptr;
+    R.beam_tx = (p->width + kBeamTile - 1) / kBeamTile;
     if (B > 1u && !(p->flags & OCTPT_RENDER_PREVIEW)) {
         // TileRenderer pass schedule (tile_renderer.rs:416-484, C20): the call covers whole passes
         if (p->flags & OCTPT_RENDER_MEGAKERNEL)
@@ -915,6 +921,22 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         ctx->wb.eye = make_float4(ctx->C.eye[0], ctx->C.eye[1], ctx->C.eye[2], none);
     }
     const WaveBuffers &B = ctx->wb;
+    // the camera rays' beam starts, once per render call: every chunk's camera rays
+    // share them (OCTPT_BEAM=0 switches them off; results are identical, ESVO iterations fewer)
+    const float *beam = nullptr;
+    if (ctx->beam) {
+        const size_t n_tiles = (size_t)R.beam_tx * ((R.H + kBeamTile - 1) / kBeamTile);
+        if (n_tiles > ctx->beam_cap) {
+            HIP_TRY(ctx, hipDeviceSynchronize());  // an earlier render may still read the table
+            if (ctx->d_beam) (void)hipFree(ctx->d_beam);
+            ctx->d_beam = nullptr;
+            ctx->beam_cap = 0;
+            HIP_TRY(ctx, hipMalloc(&ctx->d_beam, n_tiles * sizeof(float)));
+            ctx->beam_cap = n_tiles;
+        }
+        HIP_TRY(ctx, launch_beam(ctx->S, ctx->C, R, ctx->d_beam, s));
+        beam = ctx->d_beam;
+    }
     for (uint32_t c0 = 0, c1 = 0; c0 < R.spp_count; c0 = c1) {
         c1 = c0 + std::min(chunk_spp, R.spp_count - c0);
         if (R.subs) {  // a chunk ends on a pass boundary (C20): branches of one pass resolve together
@@ -930,6 +952,7 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         Rc.spp_start = R.spp_start + c0;
         Rc.spp_count = c1 - c0;
         if (R.subs) Rc.subs = R.subs + c0;
+        Rc.beam = beam;
         const uint32_t chunk_items = (uint32_t)((uint64_t)Rc.spp_count * n_px);
         HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, kCtrlWords * sizeof(uint32_t), s));
         const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
@@ -1225,6 +1248,8 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     // OCTPT_DRAIN_RAYS=n: the drain's queue threshold; 0 turns the drain off (A/B)
     const char *drain_env = std::getenv("OCTPT_DRAIN_RAYS");
     if (drain_env && *drain_env) ctx->drain_rays = (uint32_t)std::strtoul(drain_env, nullptr, 10);
+    const char *beam_env = std::getenv("OCTPT_BEAM");
+    ctx->beam = !(beam_env && beam_env[0] == '0');
     ctx->drain_models = env_u32("OCTPT_DRAIN_MODELS", 0u) != 0u;
     ctx->mem_limit = (size_t)env_u32("OCTPT_DEVICE_MEM_LIMIT", 0u) << 20;  // MiB, test hook (ensure_wave)
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
@@ -1267,6 +1292,7 @@ void octpt_destroy(octpt_ctx *ctx) {
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_subs) (void)hipFree(ctx->d_subs);
+    if (ctx->d_beam) (void)hipFree(ctx->d_beam);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_lut_float) (void)hipFree(ctx->d_lut_float);
     if (ctx->d_lut_byte) (void)hipFree(ctx->d_lut_byte);

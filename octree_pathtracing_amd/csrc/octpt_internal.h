@@ -16,6 +16,11 @@ namespace octpt {
 constexpr uint32_t kPrimNone = 0xFFFFFFFFu;
 constexpr uint32_t kPrimCuboidBit = 0x80000000u;
 constexpr uint32_t kPrimIndexMask = 0x07FFFFFFu;  // primitive indices < 2^27 (hit records pack flags above)
+// camera-ray beam starts (beam_kernel): one per kBeamTile x kBeamTile pixels (A/B knob)
+#ifndef OCTPT_BEAM_TILE
+#define OCTPT_BEAM_TILE 8
+#endif
+constexpr uint32_t kBeamTile = OCTPT_BEAM_TILE;
 constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primary rays
 constexpr uint32_t kBlock = 256;       // threads per block (4 waves)
 constexpr uint32_t kMaxDepth = 21;     // new_octree.rs:14
@@ -134,6 +139,10 @@ struct DevRender {
     // branch schedule, NULL when branch_count == 1: sub-sample k of this call is
     // subs[k] = (pass spp, pass branch count | branch << 16); spp_count then counts sub-samples
     const uint2 *subs;
+    // beam starts of the camera rays, one per kBeamTile^2 pixels of the frame (row-major, beam_tx per
+    // row), NULL = off (beam_kernel)
+    const float *beam;
+    uint32_t beam_tx;
 };
 
 // TileRenderer::get_current_branch_count (tile_renderer.rs:196-206)
@@ -229,6 +238,7 @@ int extend_blocks_per_cu(const DevScene &S);
 hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t *last_prim,
                             const float *last_normal, uint32_t n, float *t, uint32_t *prim, float *normal,
                             uint32_t *steps, hipStream_t stream);
+hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R, float *beam, hipStream_t stream);
 hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const uint8_t *lut_byte,
                           hipStream_t stream);
 hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards,

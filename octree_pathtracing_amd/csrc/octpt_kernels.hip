@@ -204,6 +204,7 @@ struct PathState {
     bool specular;
     uint32_t branch;    // branch of a split first reflection (C20), 0 = the path's own stream
     uint32_t seg_base;  // branch > 0: the segments replayed before the split (not reported)
+    float beam;         // a camera ray's beam start (octree t, beam_kernel), 0 = none
     // next-event estimation (sun sampling), used by the kNee instances only: while
     // `shadow` is set the ray is a get_direct_light_attenuation segment carrying `att`; the diffuse
     // bounce it interrupts waits in (co, cd, cn, clast, ccur), `mult` = |d_sun . n| * lum_a
@@ -748,8 +749,15 @@ __device__ __forceinline__ TraceRay make_trace_ray(const DevScene &S, v3 o, v3 d
     return t;
 }
 
+// t_start > 0 (a camera ray with a beam start, beam_kernel): no octree leaf lies within the ray's
+// tile frustum before t_start, so ESVO starts there instead of at the cube entry (Laine & Karras'
+// beam optimisation).  ESVO lands in the cell that holds the point at t_start and walks on from it;
+// the cells it skips are empty, so the first leaf it meets, and with it the hit, is the reference's.
+// t_start less a bound of ESVO's own rounding of t-values (which grows with |t_coef|, i.e. for
+// rays near-parallel to an axis), clamped to the cube exit.
 template <uint32_t kS>
-__device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk) {
+__device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk,
+                                  float t_start = 0.0f) {
     const float osc = S.octree_scale;
     // The reference zero-initialises the stack (octree_traversal.rs:69-70).  ESVO only pops to a
     // scale it pushed during the same ray (a push is skipped only when the entry already holds the
@@ -773,6 +781,12 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (rd.z > 0.0f) { E.mirror |= 4u; E.t_bias.z = 3.0f * E.t_coef.z - E.t_bias.z; }
     E.t_min = tmx(tmax3(vsub(vscale(E.t_coef, 2.0f), E.t_bias)), 0.0f);
     E.t_max = tmin3(vsub(E.t_coef, E.t_bias));
+    if (t_start > 0.0f) {
+        const float ro_m = tmx(tmx(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z));
+        const float tc_m = -tmn(tmn(E.t_coef.x, E.t_coef.y), E.t_coef.z);
+        const float margin = 0x1p-16f * (4.0f + ro_m) * tc_m;
+        E.t_min = tmx(E.t_min, tmn(t_start - margin, E.t_max));
+    }
     E.h = E.t_max;
     E.idx = 0u;
     E.pos = V(1.0f, 1.0f, 1.0f);
@@ -1291,6 +1305,7 @@ __device__ inline void new_path(const DevCamera &C, const DevRender &R, uint32_t
     ps.shadow = false;
     ps.branch = 0u;
     ps.seg_base = 0u;
+    ps.beam = 0.0f;
 }
 
 // next_intersection prologue (path_tracer.rs:438-446) + Scene::hit direction guard
@@ -1708,11 +1723,22 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
 //   ray0[q][i] = (o.xyz, last_prim)   ray1[q][i] = (d.xyz, slot | self_inward << 31)
 //   hit[i]     = (prim, t, inside | axis<<1 | (nsgn<0)<<3, -)
 //   pa[slot]   = (T.xyz, L.x)  pb[slot] = (L.y, L.z, rng, item)  pc[slot] = (cur_mat, depth | spec<<8 | segs<<16)
+//   a camera ray with a beam start: ray1 bit 30 set, ray0.w = the start t (its last_prim is kPrimNone)
+constexpr uint32_t kRayBeamBit = 0x40000000u;  // slots < 2^30 (the pool cap)
 __device__ __forceinline__ void store_ray(const WaveBuffers &B, uint32_t q, uint32_t pos, uint32_t slot,
                                           const PathState &ps) {
-    B.ray0[q][pos] = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.last_prim));
+    const bool beam = ps.beam > 0.0f && ps.path_segs == 1u;
+    B.ray0[q][pos] = make_float4(ps.o.x, ps.o.y, ps.o.z, beam ? ps.beam : __uint_as_float(ps.last_prim));
     B.ray1[q][pos] = make_float4(ps.d.x, ps.d.y, ps.d.z,
-                                 __uint_as_float(slot | (vdot(ps.d, ps.n) < 0.0f ? 0x80000000u : 0u)));
+                                 __uint_as_float(slot | (vdot(ps.d, ps.n) < 0.0f ? 0x80000000u : 0u) |
+                                                 (beam ? kRayBeamBit : 0u)));
+}
+// a ray record's last primitive and beam start
+__device__ __forceinline__ uint32_t ray_last_prim(float4 r0, float4 r1) {
+    return (__float_as_uint(r1.w) & kRayBeamBit) ? kPrimNone : __float_as_uint(r0.w);
+}
+__device__ __forceinline__ float ray_beam(float4 r0, float4 r1) {
+    return (__float_as_uint(r1.w) & kRayBeamBit) ? r0.w : 0.0f;
 }
 
 __device__ __forceinline__ void pack_path(const PathState &ps, uint32_t item, float4 &a, float4 &b, uint2 &c) {
@@ -1753,8 +1779,9 @@ __device__ __forceinline__ void load_nee(const WaveBuffers &B, uint32_t slot, Pa
 __device__ __forceinline__ void unpack_path(float4 a, float4 b, uint2 c, float4 r0, float4 r1, PathState &ps,
                                             uint32_t &item) {
     ps.o = V(r0.x, r0.y, r0.z);
-    ps.last_prim = __float_as_uint(r0.w);
+    ps.last_prim = ray_last_prim(r0, r1);
     ps.d = V(r1.x, r1.y, r1.z);
+    ps.beam = 0.0f;
     ps.T = V(a.x, a.y, a.z);
     ps.L = V(a.w, b.x, b.y);
     ps.rng = __float_as_uint(b.z);
@@ -1802,6 +1829,11 @@ __device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const W
         return false;
     }
     cnt.paths++;
+    if (R.beam) {  // the camera ray's beam start (its tile's, beam_kernel)
+        uint32_t x, y;
+        item_pixel(R, item % R.total_items, x, y);
+        ps.beam = R.beam[(y / kBeamTile) * R.beam_tx + x / kBeamTile];
+    }
     if (kSeed) B.item0[slot] = item;
     else store_path(B, slot, ps, item);
     return true;
@@ -1993,9 +2025,9 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 if (r < avail) {
                     pos = seg * B.seg_cap + c_next + r;
                     const float4 r0 = ray0[pos], r1 = ray1[pos];
-                    tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
+                    tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), ray_last_prim(r0, r1),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
-                    esvo_begin(S, tr, E, stk);
+                    esvo_begin(S, tr, E, stk, ray_beam(r0, r1));
                     active = true;
                 }
             }
@@ -2056,7 +2088,7 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
                                            const WaveBuffers &B, bool first, float4 r0, float4 r1, const uint2 *hit_rec,
                                            const float2 *huv_rec, PathState &ps, uint32_t &slot, uint32_t &item,
                                            Counters &cnt) {
-    slot = __float_as_uint(r1.w) & 0x7FFFFFFFu;
+    slot = __float_as_uint(r1.w) & (kRayBeamBit - 1u);
     if (first) {
         item = B.item0[slot];
         PathState s0;
@@ -2203,10 +2235,10 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
         for (uint32_t j = wid; j < n; j += nw) {
             float4 r0 = B.ray0[q][k * B.seg_cap + j], r1 = B.ray1[q][k * B.seg_cap + j];
             for (;;) {
-                const TraceRay tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), __float_as_uint(r0.w),
+                const TraceRay tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), ray_last_prim(r0, r1),
                                                    (__float_as_uint(r1.w) >> 31) != 0u);
                 Esvo E;
-                esvo_begin(S, tr, E, stk);
+                esvo_begin(S, tr, E, stk, ray_beam(r0, r1));
                 uint32_t prim = kPrimNone;
                 PrimHit h;
                 int rs;
@@ -2320,6 +2352,114 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
         if (out_normal) out_normal[3 * i] = out_normal[3 * i + 1] = out_normal[3 * i + 2] = 0.0f;
     }
     if (out_steps) out_steps[i] = E.iter;
+}
+
+// Beam start of the camera rays (Laine & Karras 2010, §5.2 "beam optimization"; the reference's
+// own beam-start device is get_traversal_data, octree_traversal.rs:537-714, C17).  One thread per
+// kBeamTile x kBeamTile pixel tile: every camera ray of the tile leaves the eye inside the pyramid spanned by the tile's
+// screen rectangle (new_path: pixel centre +- one jitter step, padded), so no ray of the tile meets a
+// leaf before the Euclidean distance from the eye to the nearest leaf cell that intersects the
+// pyramid.  A front-to-back depth-first walk of the octree, pruned by that distance and by the
+// pyramid's four side planes, finds it.  The start is in octree units (the ESVO t of a unit direction),
+// shrunk by a relative 2^-16 for the float evaluation; esvo_begin subtracts ESVO's own rounding bound.
+// No leaf in the pyramid: +inf (the rays start at their cube exit).  Conservative throughout: a test
+// that cannot decide keeps the cell, which can only lower the start.
+constexpr int kBeamLevels = 24;
+constexpr uint32_t kBeamVisits = 1u << 13;  // cells visited per tile; past it the tile gets no beam (0)
+#ifndef OCTPT_BEAM_LOD
+#define OCTPT_BEAM_LOD 0.0f
+#endif
+constexpr float kBeamLod = OCTPT_BEAM_LOD;
+__global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRender R, uint32_t n_tiles,
+                                                  float *__restrict__ beam) {
+    const uint32_t tile = blockIdx.x * 64u + threadIdx.x;
+    if (tile >= n_tiles) return;
+    const uint32_t tx = tile % R.beam_tx, ty = tile / R.beam_tx;
+    const uint32_t x0 = tx * kBeamTile, x1 = min(x0 + kBeamTile, R.W), y0 = ty * kBeamTile,
+                   y1 = min(y0 + kBeamTile, R.H);
+    // screen coordinates of the tile's rays (new_path: xn + dx, yn + dy), padded by 2 % + 1e-6
+    float s0 = ((float)(2u * x0) - (float)R.W) / R.dim, s1 = ((float)(2u * x1) - (float)R.W) / R.dim;
+    float t0 = ((float)(2u * (R.H - y1)) - (float)R.H) / R.dim, t1 = ((float)(2u * (R.H - y0)) - (float)R.H) / R.dim;
+    const float ps = 0.02f * (s1 - s0) + 1e-6f, pt = 0.02f * (t1 - t0) + 1e-6f;
+    s0 -= ps; s1 += ps; t0 -= pt; t1 += pt;
+    const v3 F = vscale(V(C.dir[0], C.dir[1], C.dir[2]), C.d_factor);
+    const v3 Rt = V(C.right[0], C.right[1], C.right[2]), Up = V(C.up[0], C.up[1], C.up[2]);
+    const v3 Ek[4] = {vadd(vadd(F, vscale(Rt, s0)), vscale(Up, t0)), vadd(vadd(F, vscale(Rt, s1)), vscale(Up, t0)),
+                      vadd(vadd(F, vscale(Rt, s1)), vscale(Up, t1)), vadd(vadd(F, vscale(Rt, s0)), vscale(Up, t1))};
+    const v3 Ec = vadd(vadd(F, vscale(Rt, 0.5f * (s0 + s1))), vscale(Up, 0.5f * (t0 + t1)));
+    v3 pn[4];
+    for (int k = 0; k < 4; ++k) {
+        v3 n = vcross(Ek[k], Ek[(k + 1) & 3]);
+        if (vdot(n, Ec) < 0.0f) n = vscale(n, -1.0f);
+        pn[k] = n;
+    }
+    // the eye as esvo_begin places a ray origin in octree space
+    const v3 e = vadd(vscale(V(C.eye[0], C.eye[1], C.eye[2]), S.octree_scale), V(1.0f, 1.0f, 1.0f));
+    const uint32_t om = (Ec.x < 0.0f ? 1u : 0u) | (Ec.y < 0.0f ? 2u : 0u) | (Ec.z < 0.0f ? 4u : 0u);
+    // distance from the eye to the box [lo, lo + h], or -1 when the box lies outside the pyramid
+    auto box = [&](v3 lo, float h) -> float {
+        const v3 a = vsub(lo, e), b = vsub(vadd(lo, V(h, h, h)), e);
+        const float ext = fmaxf(fmaxf(fmaxf(fabsf(a.x), fabsf(b.x)), fmaxf(fabsf(a.y), fabsf(b.y))),
+                                fmaxf(fabsf(a.z), fabsf(b.z)));
+        for (int k = 0; k < 4; ++k) {
+            const v3 n = pn[k];
+            const float mx = (fmaxf(n.x * a.x, n.x * b.x) + fmaxf(n.y * a.y, n.y * b.y)) + fmaxf(n.z * a.z, n.z * b.z);
+            const float tol = 1e-5f * ((fabsf(n.x) + fabsf(n.y)) + fabsf(n.z)) * ext;
+            if (mx < -tol) return -1.0f;
+        }
+        const float dx = a.x > 0.0f ? a.x : (b.x < 0.0f ? -b.x : 0.0f);
+        const float dy = a.y > 0.0f ? a.y : (b.y < 0.0f ? -b.y : 0.0f);
+        const float dz = a.z > 0.0f ? a.z : (b.z < 0.0f ? -b.z : 0.0f);
+        return sqrtf((dx * dx + dy * dy) + dz * dz);
+    };
+    // an octant whose cell is at most kBeamLod tile footprints wide at its distance counts as a leaf
+    // (conservative: it holds all its leaves; 0 = walk down to the leaf cells)
+    const float lod = kBeamLod * fmaxf(s1 - s0, t1 - t0) / sqrtf(vdot(F, F));
+    float best = __builtin_inff();
+    // the walk's stack in LDS, [level][thread]: octant base, mask, children still to visit (in
+    // front-to-back order: bit k = child k ^ om) and the cell's low corner
+    __shared__ uint32_t st_base[kBeamLevels][64], st_mask[kBeamLevels][64], st_rem[kBeamLevels][64];
+    __shared__ float st_lx[kBeamLevels][64], st_ly[kBeamLevels][64], st_lz[kBeamLevels][64];
+    const uint32_t t = threadIdx.x;
+    auto order = [&](uint32_t m) {  // present children, permuted so that bit k = child k ^ om
+        uint32_t pm = m & 0xFFu;
+        if (om & 1u) pm = ((pm & 0x55u) << 1) | ((pm >> 1) & 0x55u);
+        if (om & 2u) pm = ((pm & 0x33u) << 2) | ((pm >> 2) & 0x33u);
+        if (om & 4u) pm = ((pm & 0x0Fu) << 4) | ((pm >> 4) & 0x0Fu);
+        return pm;
+    };
+    bool exhausted = S.depth >= (uint32_t)kBeamLevels;
+    if (!exhausted && box(V(1.0f, 1.0f, 1.0f), 1.0f) >= 0.0f) {
+        int lv = 0;
+        st_base[0][t] = S.root;
+        st_mask[0][t] = S.root_mask;
+        st_rem[0][t] = order(S.root_mask);
+        st_lx[0][t] = st_ly[0][t] = st_lz[0][t] = 1.0f;
+        uint32_t visits = 0u;
+        while (lv >= 0) {
+            const uint32_t rem = st_rem[lv][t];
+            if (rem == 0u) { --lv; continue; }
+            if (++visits > kBeamVisits) { exhausted = true; break; }
+            st_rem[lv][t] = rem & (rem - 1u);
+            const uint32_t ci = (uint32_t)(__ffs(rem) - 1) ^ om;
+            const uint32_t m = st_mask[lv][t], kind = (m >> ci) & 0x101u;
+            const float h = __uint_as_float((126u - (uint32_t)lv) << 23);  // 2^-(lv + 1)
+            const v3 lo = V(st_lx[lv][t] + ((ci & 1u) ? h : 0.0f), st_ly[lv][t] + ((ci & 2u) ? h : 0.0f),
+                            st_lz[lv][t] + ((ci & 4u) ? h : 0.0f));
+            const float d = box(lo, h);
+            if (d < 0.0f || d >= best) continue;
+            if (kind == 0x101u || lv + 1 >= kBeamLevels || h <= lod * d) { best = d; continue; }  // leaf / small cell
+            const uint2 slot = S.node_child[st_base[lv][t] + __popc(m & ((1u << ci) - 1u))];
+            ++lv;
+            st_base[lv][t] = slot.x;
+            st_mask[lv][t] = slot.y;
+            st_rem[lv][t] = order(slot.y);
+            st_lx[lv][t] = lo.x;
+            st_ly[lv][t] = lo.y;
+            st_lz[lv][t] = lo.z;
+        }
+    }
+    beam[tile] = exhausted ? 0.0f : best * (1.0f - 0x1p-16f);
 }
 
 __global__ void tonemap_kernel(const float4 *__restrict__ accum, uchar4 *__restrict__ out, uint32_t n,
@@ -2483,6 +2623,12 @@ hipError_t launch_intersect(const DevScene &S0, const float *rays, const uint32_
     hipLaunchKernelGGL(S.has_blocks ? intersect_kernel<kPrimsBlocks> : intersect_kernel<kPrimsModels>, dim3(grid),
                        dim3(kBlock), render_lds_bytes(S.depth), stream, S, rays, last_prim, last_normal, n, t, prim,
                        normal, steps);
+    return hipGetLastError();
+}
+
+hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R, float *beam, hipStream_t stream) {
+    const uint32_t n = R.beam_tx * ((R.H + kBeamTile - 1u) / kBeamTile);
+    hipLaunchKernelGGL(beam_kernel, dim3((n + 63u) / 64u), dim3(64), 0, stream, S, C, R, n, beam);
     return hipGetLastError();
 }
 

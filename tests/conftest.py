@@ -1,3 +1,4 @@
+import os
 import sys
 from pathlib import Path
 
@@ -5,6 +6,14 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
+
+# The camera rays' beam start skips ESVO iterations over empty cells, so a render with
+# it counts fewer ESVO iterations than the oracle, which restates the reference's walk from the cube
+# entry.  The oracle-parity tests therefore run without it, which keeps the per-render ESVO iteration
+# total an exact check of the traversal; tests/test_gpu_beam.py shows that renders with the beam equal
+# those without it in everything else, bit for bit (and smoke() checks the shipped default against
+# the oracle).
+os.environ.setdefault("OCTPT_BEAM", "0")
 
 
 def pytest_configure(config):

@@ -1,0 +1,129 @@
+"""The camera rays' beam start (beam_kernel): each 8x8 tile's camera rays begin ESVO at
+the distance from the eye to the nearest leaf cell inside the tile's pyramid, not at the cube entry.
+The cells skipped are empty, so a render with the beam equals the render without it (OCTPT_BEAM=0,
+itself checked against the oracle by the parity suite) bit for bit: radiance, per-pixel segment
+counts and every statistic except the ESVO iteration total, which can only fall.  Covered: sphere,
+box, block-model and block-value scenes, interior cameras, sun sampling, branch counts, and a pool
+small enough that regenerated camera rays carry the beam through the shade kernel."""
+import os
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import gpu_render, renderer, torch_cuda  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+SAME = ("paths", "segments", "sphere_tests", "cuboid_tests", "shade_events", "texel_reads", "block_tests")
+
+
+def _renderer_with(env):
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)  # read when the context is created
+    try:
+        return HipRenderer(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def beam(torch_cuda):
+    r = _renderer_with({"OCTPT_BEAM": "1"})
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def beam_small_pool(torch_cuda):
+    r = _renderer_with({"OCTPT_BEAM": "1", "OCTPT_POOL": "65536", "OCTPT_CHUNK": "200000"})
+    yield r
+    r.close()
+
+
+def _same(a, b):
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32)), "radiance"
+    assert np.array_equal(a[1], b[1]), "segment counts"
+    for k in SAME:
+        assert a[2][k] == b[2][k], k
+    assert a[2]["esvo_steps"] <= b[2]["esvo_steps"]
+
+
+@pytest.mark.parametrize("name,res,variant,bc", [
+    ("C3", (480, 270, 4), None, 1), ("C2", (320, 180, 8), None, 1), ("C4", (256, 144, 2), None, 1),
+    ("C5", (256, 144, 2), None, 1), ("C5b", (256, 144, 2), None, 1), ("blocks", None, None, 1),
+    ("blocks-b", None, None, 1), ("C3-in", (320, 180, 2), None, 1), ("C5-fp", (256, 144, 2), None, 1),
+    ("C5b-fp", (256, 144, 2), None, 1), ("C5s-small", (256, 144, 4), "fast", 1), ("tiny", None, "hq", 1),
+    ("C2", (160, 90, 4), "nee_importance", 1), ("tiny", None, None, 4), ("C1", None, None, 1),
+    ("C1-as-is", None, None, 1)])
+def test_beam_equals_no_beam(torch_cuda, renderer, beam, beam_small_pool, name, res, variant, bc):
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config(name)
+    if res:
+        rs.width, rs.height, rs.spp = res
+    if variant:
+        S.with_sun_variant(sc, variant)
+    if bc > 1:
+        rs.spp = 8
+    off = gpu_render(torch_cuda, renderer, sc, cam, rs, branch_count=bc)
+    on = gpu_render(torch_cuda, beam, sc, cam, rs, branch_count=bc)
+    _same(on, off)
+    small = gpu_render(torch_cuda, beam_small_pool, sc, cam, rs, branch_count=bc)
+    _same(small, off)
+    assert small[2]["esvo_steps"] == on[2]["esvo_steps"]
+
+
+def test_beam_skips_iterations(torch_cuda, renderer, beam):
+    """On the headline scene the beam removes a large share of the camera rays' iterations."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config("C3")
+    rs.width, rs.height, rs.spp, rs.max_depth = 480, 270, 2, 1
+    off = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    on = gpu_render(torch_cuda, beam, sc, cam, rs)
+    _same(on, off)
+    assert on[2]["esvo_steps"] < 0.95 * off[2]["esvo_steps"], (on[2]["esvo_steps"], off[2]["esvo_steps"])
+
+
+def test_beam_shards_and_progressive(torch_cuda, renderer, beam):
+    """Shards (compact tile buffers) and a progressive split read the frame's beam table by pixel."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config("C3")
+    rs.width, rs.height, rs.spp = 200, 120, 4
+    full = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    for k in range(3):
+        a = gpu_render(torch_cuda, beam, sc, cam, rs, shard=(k, 3), compact=True)
+        b = gpu_render(torch_cuda, renderer, sc, cam, rs, shard=(k, 3), compact=True)
+        assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+        assert np.array_equal(a[1], b[1])
+    rs2 = S.make_config("C3")[2]
+    rs2.width, rs2.height, rs2.spp = 200, 120, 2
+    first = gpu_render(torch_cuda, beam, sc, cam, rs2)
+    second = gpu_render(torch_cuda, beam, sc, cam, rs2, spp_start=2, accum=first[0])
+    assert np.array_equal(second[0].view(np.uint32), full[0].view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", list(range(1000, 1032)) + list(range(2000, 2016)) + list(range(3000, 3064)))
+def test_beam_fuzz(torch_cuda, renderer, beam, seed):
+    """tests/test_gpu_fuzz.py's random scenes, octree forms and cameras (inside and outside the cube,
+    fields of view 30-100 degrees), plus 64 more seeds: the beam changes nothing but the iteration
+    total.  Seeds >= 3000 render at up to 4x the fuzz resolution, so that tiles hold many pixels."""
+    from tests.test_gpu_fuzz import fuzz_scene
+
+    kind = 4 if 2000 <= seed < 2016 or (seed >= 3000 and seed % 5 == 0) else None
+    sc, cam, rs, tag = fuzz_scene(seed, kind=kind)
+    if seed >= 3000:
+        rs.width, rs.height = rs.width * 4, rs.height * 4
+    off = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    on = gpu_render(torch_cuda, beam, sc, cam, rs)
+    try:
+        _same(on, off)
+    except AssertionError as e:
+        raise AssertionError(f"{tag}: {e}") from e
