@@ -228,6 +228,8 @@ typedef struct octpt_render_params {
 #define OCTPT_STAT_ISSUED_BYTES 8
 #define OCTPT_STAT_COUNT 9
 typedef struct octpt_stats {
+    /* esvo_steps: ESVO iterations executed; camera rays start at their tile's beam start, so
+       this is the reference walk's count only with OCTPT_BEAM=0 -- every other field is the same either way */
     uint64_t paths, segments, esvo_steps, sphere_tests, cuboid_tests, shade_events, texel_reads;
     uint64_t launches;
     double kernel_ms; /* HIP-event time of the render calls since the last reset */
