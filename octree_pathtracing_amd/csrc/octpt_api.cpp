@@ -79,7 +79,7 @@ struct octpt_ctx {
     std::vector<uint2> h_subs;
     uint2 *d_subs = nullptr;
     size_t subs_cap = 0;
-    // beam starts of the camera rays, one per 8x8 tile (beam_kernel), grow-only
+    // beam starts of the camera rays, one per kBeamTile^2 pixels (beam_kernel), grow-only
     float *d_beam = nullptr;
     size_t beam_cap = 0;
     uint32_t launch_seq = 0;

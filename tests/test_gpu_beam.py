@@ -1,4 +1,4 @@
-"""The camera rays' beam start (beam_kernel): each 8x8 tile's camera rays begin ESVO at
+"""The camera rays' beam start (beam_kernel): each beam tile's (4x4 pixels) camera rays begin ESVO at
 the distance from the eye to the nearest leaf cell inside the tile's pyramid, not at the cube entry.
 The cells skipped are empty, so a render with the beam equals the render without it (OCTPT_BEAM=0,
 itself checked against the oracle by the parity suite) bit for bit: radiance, per-pixel segment
@@ -127,3 +127,17 @@ def test_beam_fuzz(torch_cuda, renderer, beam, seed):
         _same(on, off)
     except AssertionError as e:
         raise AssertionError(f"{tag}: {e}") from e
+
+
+def test_rcp_exhaustive(torch_cuda):
+    """esvo_begin's t_coef = 1 / -|d| comes from csrc/octpt_rcp.h's hardware reciprocal + one fused Newton
+    step; tools/rcp_check compares it with the correctly rounded division for every float |d| in
+    [2^-23, 2] (ESVO's clamp to the unit vector's range), both signs."""
+    import subprocess
+    from pathlib import Path
+
+    exe = Path(__file__).resolve().parents[1] / "tools" / "rcp_check"
+    assert exe.exists(), "build it with __graft_entry__.build()"
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "mismatches 0" in p.stdout, p.stdout
