@@ -2376,6 +2376,8 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
 // No leaf in the pyramid: +inf (the rays start at their cube exit).  Conservative throughout: a test
 // that cannot decide keeps the cell, which can only lower the start.
 constexpr int kBeamLevels = 24;
+static_assert(kTile % kBeamTile == 0, "beam tiles nest in the 8x8 render tiles");
+constexpr uint32_t kBeamSub = (kTile / kBeamTile) * (kTile / kBeamTile);  // beam tiles per render tile
 constexpr uint32_t kBeamVisits = 1u << 13;  // cells visited per tile; past it the tile gets no beam (0)
 #ifndef OCTPT_BEAM_LOD
 #define OCTPT_BEAM_LOD 0.0f
@@ -2383,11 +2385,16 @@ constexpr uint32_t kBeamVisits = 1u << 13;  // cells visited per tile; past it t
 constexpr float kBeamLod = OCTPT_BEAM_LOD;
 __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRender R, uint32_t n_tiles,
                                                   float *__restrict__ beam) {
-    const uint32_t tile = blockIdx.x * 64u + threadIdx.x;
-    if (tile >= n_tiles) return;
-    const uint32_t tx = tile % R.beam_tx, ty = tile / R.beam_tx;
-    const uint32_t x0 = tx * kBeamTile, x1 = min(x0 + kBeamTile, R.W), y0 = ty * kBeamTile,
-                   y1 = min(y0 + kBeamTile, R.H);
+    // thread i: beam tile i % kBeamSub of the shard's render tile i / kBeamSub (item_pixel's tile order),
+    // so a rank of N computes only its own tiles' starts
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= n_tiles) return;
+    const uint32_t rt = R.shard_index + (i / kBeamSub) * R.shard_count, sub = i % kBeamSub;
+    const uint32_t x0 = (rt % R.tiles_x) * kTile + (sub % (kTile / kBeamTile)) * kBeamTile,
+                   y0 = (rt / R.tiles_x) * kTile + (sub / (kTile / kBeamTile)) * kBeamTile;
+    if (x0 >= R.W || y0 >= R.H) return;  // no pixel of the image: never read
+    const uint32_t tile = (y0 / kBeamTile) * R.beam_tx + x0 / kBeamTile;
+    const uint32_t x1 = min(x0 + kBeamTile, R.W), y1 = min(y0 + kBeamTile, R.H);
     // screen coordinates of the tile's rays (new_path: xn + dx, yn + dy), padded by 2 % + 1e-6
     float s0 = ((float)(2u * x0) - (float)R.W) / R.dim, s1 = ((float)(2u * x1) - (float)R.W) / R.dim;
     float t0 = ((float)(2u * (R.H - y1)) - (float)R.H) / R.dim, t1 = ((float)(2u * (R.H - y0)) - (float)R.H) / R.dim;
@@ -2638,7 +2645,7 @@ hipError_t launch_intersect(const DevScene &S0, const float *rays, const uint32_
 }
 
 hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R, float *beam, hipStream_t stream) {
-    const uint32_t n = R.beam_tx * ((R.H + kBeamTile - 1u) / kBeamTile);
+    const uint32_t n = R.shard_tiles * kBeamSub;  // the shard's render tiles' beam tiles
     hipLaunchKernelGGL(beam_kernel, dim3((n + 63u) / 64u), dim3(64), 0, stream, S, C, R, n, beam);
     return hipGetLastError();
 }
