@@ -19,7 +19,7 @@
 #include "octpt_rcp.h"
 
 #ifndef OCTPT_RCP_FAST
-#define OCTPT_RCP_FAST 0  // esvo_begin's t_coef by rcp_rn (A/B: -DOCTPT_RCP_FAST=0, the division)
+#define OCTPT_RCP_FAST 1  // esvo_begin's t_coef by rcp_rn (A/B: -DOCTPT_RCP_FAST=0, the division: extend +0.2..0.6 %)
 #endif
 
 namespace octpt {
@@ -780,7 +780,7 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (fabsf(rd.z) < OCTREE_EPSILON) rd.z = __uint_as_float(epsb | (__float_as_uint(rd.z) & 0x80000000u));
 #if OCTPT_RCP_FAST
     // the correctly rounded quotients from v_rcp_f32 + one fused Newton step (octpt_rcp.h: compared with
-    // the division for every |rd| in [2^-23, 2] by tools/rcp_check.hip), 3 instead of ~11 instructions each
+    // the division for every |rd| in [2^-23, 2^126] by tools/rcp_check.hip), 3 instead of ~11 instructions each
     E.t_coef = V(rcp_rn(-fabsf(rd.x)), rcp_rn(-fabsf(rd.y)), rcp_rn(-fabsf(rd.z)));  // [C13]
 #else
     E.t_coef = V(1.0f / -fabsf(rd.x), 1.0f / -fabsf(rd.y), 1.0f / -fabsf(rd.z));  // [C13]

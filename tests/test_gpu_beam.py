@@ -132,7 +132,7 @@ def test_beam_fuzz(torch_cuda, renderer, beam, seed):
 def test_rcp_exhaustive(torch_cuda):
     """esvo_begin's t_coef = 1 / -|d| comes from csrc/octpt_rcp.h's hardware reciprocal + one fused Newton
     step; tools/rcp_check compares it with the correctly rounded division for every float |d| in
-    [2^-23, 2] (ESVO's clamp to the unit vector's range), both signs."""
+    [2^-23, 2^126] (ESVO clamps |d| to 2^-23; every quotient is a normal float), both signs."""
     import subprocess
     from pathlib import Path
 

@@ -1,6 +1,6 @@
 // Exhaustive check of octpt::rcp_rn (csrc/octpt_rcp.h) against the correctly rounded division 1.0f / a
 // (this file is built with -fhip-fp32-correctly-rounded-divide-sqrt, as liboctpt is) for every float a
-// with |a| in [2^-23, 2], both signs.  Prints the number of values checked and of mismatches, exit 0 iff
+// with |a| in [2^-23, 2^126], both signs (every quotient a normal float).  Prints the number of values checked and of mismatches, exit 0 iff
 // there are none.  Built by __graft_entry__.build(); run by tests/test_gpu_beam.py on the GPU.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -21,7 +21,7 @@ __global__ void check(uint32_t lo, uint32_t n, unsigned long long *bad, uint32_t
 
 int main() {
     const uint32_t lo = 0x34000000u;  // 2^-23
-    const uint32_t hi = 0x40000000u;  // 2.0
+    const uint32_t hi = 0x7E800000u;  // 2^126
     const uint32_t n = hi - lo + 1u;
     unsigned long long *bad;
     uint32_t *first;
