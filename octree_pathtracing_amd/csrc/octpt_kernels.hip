@@ -2378,7 +2378,10 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
 constexpr int kBeamLevels = 24;
 static_assert(kTile % kBeamTile == 0, "beam tiles nest in the 8x8 render tiles");
 constexpr uint32_t kBeamSub = (kTile / kBeamTile) * (kTile / kBeamTile);  // beam tiles per render tile
-constexpr uint32_t kBeamVisits = 1u << 13;  // cells visited per tile; past it the tile gets no beam (0)
+#ifndef OCTPT_BEAM_VISITS
+#define OCTPT_BEAM_VISITS (1u << 13)
+#endif
+constexpr uint32_t kBeamVisits = OCTPT_BEAM_VISITS;  // cells visited per tile; past it the tile gets no beam (0)
 #ifndef OCTPT_BEAM_LOD
 #define OCTPT_BEAM_LOD 0.0f
 #endif
