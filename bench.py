@@ -190,6 +190,50 @@ def issued_probe(sc, cam, rs, dev_idx: int, ext_s: float):
                      "one render of the same step, divided by the timed library's mean extend launch time"}
 
 
+def capi_devices(spec: str, n_visible: int) -> list:
+    """--capi-devices: "N" = the first N visible devices (repeating device ids when fewer are visible, as on
+    a one-GPU box), or an explicit comma-separated list of HIP device ids."""
+    if "," in spec:
+        return [int(x) for x in spec.split(",")]
+    return [i % max(n_visible, 1) for i in range(int(spec))]
+
+
+def capi_multi_measure(sc, cam, rs, devices, steps: int, warmup: int) -> dict:
+    """The multi-device path a Rust host calls (octpt_create_multi): one process, one context
+    over `devices`, whole frames through octpt_render_device into a frame buffer on devices[0] (tiles dealt
+    over the entries, gathered with peer copies inside liboctpt).  Whole-job Mrays/s over the timed steps."""
+    import torch
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    W, H = rs.width, rs.height
+    r = HipRenderer(devices=devices)
+    try:
+        r.set_scene(sc)
+        r.set_camera(cam)
+        r.max_depth, r.seed = rs.max_depth, rs.seed
+        dev = torch.device("cuda", devices[0])
+        acc = torch.zeros((W * H, 4), dtype=torch.float32, device=dev)
+        p = r.params(W, H, 0, rs.spp)
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream().cuda_stream
+            for _ in range(warmup):
+                acc[:, 3] = 1.0
+                r.render_device(p, acc.data_ptr(), None, stream)
+            torch.cuda.synchronize()
+            r.reset_stats()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                r.render_device(p, acc.data_ptr(), None, stream)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+        st = r.stats()
+    finally:
+        r.close()
+    return {"value": round(st["segments"] / dt / 1e6, 2), "unit": "Mrays/s", "devices": list(devices),
+            "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "segments": st["segments"],
+            "path": "octpt_create_multi + octpt_render_device (one process, peer-copy gather inside liboctpt)"}
+
+
 def scene_contents(sc) -> str:
     if sc.blocks is not None:  # block-value leaves (DESIGN.md C23)
         return f"{len(sc.cells)} voxel cells as block-value leaves ({len(sc.blocks)} block kinds)"
@@ -212,6 +256,12 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: host-staged gather (rehearses N ranks on fewer GPUs); nccl = RCCL over xGMI")
     ap.add_argument("--dump-frame", default=None, help="rank 0 saves the gathered frame (.npy) after the last step")
+    ap.add_argument("--capi-devices", default=None,
+                    help="one process, one multi-device context (octpt_create_multi) over N devices or a list of "
+                         "HIP ids: the C-ABI path a Rust host calls (DESIGN.md §9); ids repeat on a one-GPU box")
+    ap.add_argument("--no-capi-multi", action="store_true",
+                    help="with N > 1 ranks, skip rank 0's extra measurement of the same frame through one "
+                         "multi-device context over the N devices")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -252,7 +302,8 @@ def main():
     if args.spp:
         rs.spp = args.spp
     W, H = rs.width, rs.height
-    r = HipRenderer(device=dev_idx)
+    multi = capi_devices(args.capi_devices, n_dev) if (args.capi_devices and world == 1) else None
+    r = HipRenderer(devices=multi) if multi else HipRenderer(device=dev_idx)
     r.set_scene(sc)
     r.set_camera(cam)
     r.max_depth, r.seed = rs.max_depth, rs.seed
@@ -267,6 +318,10 @@ def main():
     gbuf_dev = torch.zeros((world * stride, 4), dtype=torch.float32, device=dev) if (host_staged and rank == 0) else None
     frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev) if (world > 1 and rank == 0) else None
     params = r.params(W, H, 0, rs.spp, rank, world, compact=True, kernel_timing=True)
+    if multi:  # the whole frame in image order on devices[0]: the multi-device context gathers it itself
+        accum = torch.zeros((W * H, 4), dtype=torch.float32, device=dev)
+        accum[:, 3] = 1.0
+        params = r.params(W, H, 0, rs.spp, kernel_timing=True)
 
     def unshard(g):
         stream = torch.cuda.current_stream().cuda_stream
@@ -335,7 +390,8 @@ def main():
                         f"{rs.spp} spp, max_depth {rs.max_depth}, seed {rs.seed}",
             "resolution": [W, H],
             "spp": rs.spp,
-            "parallelism": (f"tiles{world}" + ("-gloo" if host_staged else "")) if world > 1 else "single",
+            "parallelism": ((f"tiles{world}" + ("-gloo" if host_staged else "")) if world > 1
+                            else f"capi-multi{len(multi)}" if multi else "single"),
             "paths_per_step": W * H * rs.spp,
             "segments_per_step": seg // max(args.steps, 1),
         },
@@ -362,7 +418,19 @@ def main():
         },
         "stats_rank0": {k: v for k, v in st.items() if k != "kernel_ms"},
     }
-    if rank == 0 and world == 1 and not args.no_issued:
+    if multi:
+        out["config"]["capi_devices"] = multi
+    if world > 1 and not args.no_capi_multi and args.dist_backend == "nccl":
+        # the same frame through the C-ABI path a Rust host calls: one process (rank 0), one multi-device
+        # context over the N devices, tiles gathered inside liboctpt; the other ranks wait
+        dist.barrier()
+        if rank == 0:
+            try:
+                out["capi_multi"] = capi_multi_measure(sc, cam, rs, list(range(world)), args.steps, args.warmup)
+            except Exception as e:  # reported, never fatal to the bench line
+                out["capi_multi"] = {"error": f"{type(e).__name__}: {e}"}
+        dist.barrier()
+    if rank == 0 and world == 1 and not args.no_issued and not multi:
         out["roofline"]["issued"] = issued_probe(sc, cam, rs, dev_idx, ext_s)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sc, cam, rs, args.cpu_seconds, args.cpu_threads)
@@ -371,7 +439,9 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
         if args.dump_frame:  # the frame in image order (a single rank's buffer is tile-major too)
-            if world == 1:
+            if multi:
+                frame = accum
+            elif world == 1:
                 frame = torch.zeros((H * W, 4), dtype=torch.float32, device=dev)
                 r.unshard_device(W, H, 1, accum.data_ptr(), stride, frame.data_ptr(),
                                  torch.cuda.current_stream().cuda_stream)

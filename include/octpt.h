@@ -15,6 +15,10 @@
  *    the caller until octpt_frame_release.
  *  - There is no CPU fallback: without a usable gfx950 device octpt_create fails
  *    with OCTPT_ERR_DEVICE.
+ *  - "Drop-in" is not literal: a Rust host binding this header adds two accessors to the reference
+ *    (Octant::raw_parts in src/octree/new_octree.rs, Sun::octpt_args in src/scene/mod.rs) and supplies the
+ *    block table (block value -> face materials / model) that its resource manager resolves and Scene does
+ *    not hold.  src/app and the rest of src/scene are untouched.
  */
 #ifndef OCTPT_H
 #define OCTPT_H
@@ -26,7 +30,7 @@
 extern "C" {
 #endif
 
-#define OCTPT_ABI_VERSION 3u
+#define OCTPT_ABI_VERSION 4u
 
 typedef int32_t octpt_status;
 #define OCTPT_OK 0
@@ -247,6 +251,9 @@ typedef struct octpt_stats {
     uint64_t pool_slots;  /* path slots held by the wavefront state (after any out-of-memory fallback) */
     uint64_t chunk_items; /* (pixel, sample) items per chunk held (likewise) */
     uint64_t wave_allocs; /* wavefront-state (re)allocations since the context was created */
+    /* camera rays whose beam start reached the reference's step cap and were traced again from the
+     * cube entry (their iterations before the restart are in esvo_steps too) */
+    uint64_t beam_restarts;
 } octpt_stats;
 
 /* --- library / context ------------------------------------------------------ */
@@ -255,6 +262,17 @@ uint32_t octpt_abi_version(void);
 int32_t octpt_device_count(void);
 /* RenderingBackend construction (gpu_renderer.rs:151-200) on HIP device `device` */
 octpt_status octpt_create(int32_t device, octpt_ctx **out);
+/* A context over several GPUs of one node (SURVEY.md §8(b) device list, §8(e) tile split):
+ * devices[0 .. n) are HIP device ids, n <= 64; an id may repeat (two entries on one GPU).  Every entry
+ * point takes such a context: the scene is replicated on every entry, a render deals the 8x8 tiles of the
+ * call's shard round-robin over the entries (each renders its tiles concurrently, on a host thread of its
+ * own) and gathers them with peer copies into the caller's buffers, which live on devices[0]
+ * (octpt_render_device's d_accum / d_seg_count and stream).  Results are bit-identical to one device's.
+ * octpt_intersect runs on devices[0]; octpt_stats sums the entries' counters, kernel_ms is the render
+ * calls' wall time.  n == 1 is octpt_create(devices[0]). */
+octpt_status octpt_create_multi(const int32_t *devices, uint32_t n, octpt_ctx **out);
+/* device entries of a context (1 for octpt_create; 0 for NULL) */
+uint32_t octpt_device_entries(const octpt_ctx *ctx);
 void octpt_destroy(octpt_ctx *ctx);
 /* last error message of this context (never NULL) */
 const char *octpt_last_error(const octpt_ctx *ctx);
@@ -307,7 +325,9 @@ octpt_status octpt_unshard_device(octpt_ctx *ctx, uint32_t width, uint32_t heigh
 uint32_t octpt_shard_pixels(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count);
 
 /* Batch closest-hit query = Scene::hit (scene/mod.rs:172-187) with the octree traversal
- * (octree_traversal.rs:54-302) restored.  rays: n*6 floats (origin, unit direction), host.
+ * (octree_traversal.rs:54-302) restored.  rays: n*6 floats (origin, unit direction), host; every
+ * component finite and each direction component |d| <= 2^126 (else INVALID_ARG: ESVO's 1 / -|d| is
+ * exact in that range; components below 2^-23 are clamped to it as the reference does).
  * last_prim / last_normal (nullable): self-intersection key per ray.
  * Outputs (host): t (world, +inf on miss), prim (0xFFFFFFFF on miss; in a block-value scene, C23, the
  * block id, or 0x40000000 | quad for a block model's quad), normal n*3 (nullable), esvo steps (nullable). */

@@ -13,7 +13,7 @@ from pathlib import Path
 LIB_DIR = Path(__file__).resolve().parent / "lib"
 LIB_PATH = LIB_DIR / "liboctpt.so"
 
-OCTPT_ABI_VERSION = 3
+OCTPT_ABI_VERSION = 4
 
 OK = 0
 ERR_INVALID_ARG = 1
@@ -175,7 +175,7 @@ class Stats(C.Structure):
                 ("extend_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("extend_ms", C.c_double),
                 ("shade_ms", C.c_double), ("build_ms", C.c_double), ("block_tests", C.c_uint64),
                 ("issued_bytes", C.c_uint64), ("drain", C.c_uint64 * STAT_COUNT), ("pool_slots", C.c_uint64),
-                ("chunk_items", C.c_uint64), ("wave_allocs", C.c_uint64)]
+                ("chunk_items", C.c_uint64), ("wave_allocs", C.c_uint64), ("beam_restarts", C.c_uint64)]
 
     def as_dict(self) -> dict:
         d = {name: getattr(self, name) for name, _ in self._fields_}
@@ -195,6 +195,8 @@ SIGNATURES = {
     "octpt_abi_version": (_u32, []),
     "octpt_device_count": (_i32, []),
     "octpt_create": (_i32, [_i32, C.POINTER(_vp)]),
+    "octpt_create_multi": (_i32, [_vp, _u32, C.POINTER(_vp)]),
+    "octpt_device_entries": (_u32, [_vp]),
     "octpt_destroy": (None, [_vp]),
     "octpt_last_error": (C.c_char_p, [_vp]),
     "octpt_scene_upload": (_i32, [_vp, C.POINTER(SceneDesc)]),

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <thread>
@@ -122,10 +123,19 @@ struct octpt_ctx {
     uint64_t chunk_cap = kDefaultChunkPaths;  // (pixel, sample) items per chunk (OCTPT_CHUNK)
     // one asynchronous frame may be in flight; device-touching calls join it first
     octpt_frame *inflight = nullptr;
+    // multi-device context (octpt_create_multi): one child context per device entry; this context's own
+    // device is the first entry's, where the caller's buffers live.  Empty for octpt_create.
+    std::vector<octpt_ctx *> sub;
+    // multi-device renders: the staged compact tile buffers (this context: every entry's, side by side on
+    // the first device; a child: its own), grow-only
+    float4 *m_acc = nullptr;
+    uint32_t *m_seg = nullptr;
+    size_t m_acc_cap = 0, m_seg_cap = 0;
 };
 
 struct octpt_frame {
     octpt_ctx *ctx = nullptr;
+    octpt_render_params params{};  // the call's parameters (a multi-device context re-derives each entry's)
     std::thread worker;
     std::atomic<bool> finished{false};
     std::atomic<bool> cancel_requested{false};
@@ -1036,6 +1046,104 @@ octpt_status enqueue_render(octpt_ctx *ctx, const DevRender &R, float4 *d_accum,
     return st;
 }
 
+// ---------------- multi-device contexts (octpt_create_multi) ----------------
+// A multi-device context forwards every call to one child context per device entry, each a complete
+// single-device context (its own scene replica, stream and wavefront state).  A render deals the caller's
+// 8x8 tiles round-robin over the entries (multi_slot: the children's own shards of the kernels' tile
+// split), runs each child on a host thread of its own (the wavefront loop is host-steered), and moves the
+// tiles between the caller's buffers on the first device and the children's compact buffers with peer
+// copies (hipMemcpyPeerAsync: xGMI DMA between MI355X devices; a plain device copy when an entry repeats
+// a device).  Per-pixel RNG streams make the result bit-identical to one device's.
+bool is_multi(const octpt_ctx *ctx) { return !ctx->sub.empty(); }
+
+// fn(i) for every child i, one host thread each; the first failing entry's status and message are returned
+template <class F>
+octpt_status for_each_sub(octpt_ctx *ctx, F fn) {
+    const size_t n = ctx->sub.size();
+    std::vector<octpt_status> st(n, OCTPT_OK);
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (size_t i = 0; i < n; ++i)
+        th.emplace_back([&st, &fn, ctx, i]() {
+            try {
+                st[i] = fn(i);
+            } catch (...) {
+                st[i] = fail(ctx->sub[i], OCTPT_ERR_INTERNAL, "unexpected exception");
+            }
+        });
+    for (auto &t : th) t.join();
+    for (size_t i = 0; i < n; ++i)
+        if (st[i] != OCTPT_OK)
+            return fail(ctx, st[i], "device entry " + std::to_string(i) + " (HIP device " +
+                                        std::to_string(ctx->sub[i]->device) + "): " + ctx->sub[i]->err);
+    return OCTPT_OK;
+}
+
+// grow-only device buffer of n elements on the current device
+template <class T>
+octpt_status grow_buf(octpt_ctx *ctx, T *&p, size_t &cap, size_t n) {
+    if (n <= cap) return OCTPT_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(ctx, hipMalloc(&p, n * sizeof(T)));
+    cap = n;
+    return OCTPT_OK;
+}
+
+// One render call over every device entry: scatter the caller's running mean (and segment counts) into the
+// entries' compact tile buffers, render each entry's shard, gather back.  R is the call's layout (on the
+// first device, stream s); the caller's buffers are read and written on s, the entries work on their own
+// streams.  kernel_ms accumulates the call's wall time (the entries run concurrently).
+octpt_status multi_render(octpt_ctx *ctx, const octpt_render_params &p, const DevRender &R, float4 *d_accum,
+                          uint32_t *d_seg, hipStream_t s, const std::atomic<bool> *cancel) {
+    if (R.spp_count == 0 || R.total_items == 0) return OCTPT_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t n = (uint32_t)ctx->sub.size();
+    const size_t stride = (size_t)((R.shard_tiles + n - 1) / n) * 64u;  // the largest entry's pixels
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    octpt_status st = grow_buf(ctx, ctx->m_acc, ctx->m_acc_cap, stride * n);
+    if (st == OCTPT_OK && d_seg) st = grow_buf(ctx, ctx->m_seg, ctx->m_seg_cap, stride * n);
+    if (st != OCTPT_OK) return st;
+    HIP_TRY(ctx, launch_multi_stage(R, n, (uint32_t)stride, d_accum, d_seg, ctx->m_acc, ctx->m_seg, true, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    const bool megakernel = (p.flags & OCTPT_RENDER_MEGAKERNEL) != 0;
+    st = for_each_sub(ctx, [&](size_t i) -> octpt_status {
+        octpt_ctx *c = ctx->sub[i];
+        HIP_TRY(c, hipSetDevice(c->device));
+        octpt_render_params pi = p;  // entry i's shard of the caller's shard (multi_slot)
+        pi.shard_index = p.shard_index + (uint32_t)i * p.shard_count;
+        pi.shard_count = p.shard_count * n;
+        pi.flags |= OCTPT_RENDER_SHARD_COMPACT;
+        DevRender Ri{};
+        octpt_status r = make_render(c, &pi, Ri);
+        if (r != OCTPT_OK || Ri.total_items == 0) return r;
+        const size_t np = Ri.total_items;
+        if ((r = grow_buf(c, c->m_acc, c->m_acc_cap, np)) != OCTPT_OK) return r;
+        if (d_seg && (r = grow_buf(c, c->m_seg, c->m_seg_cap, np)) != OCTPT_OK) return r;
+        float4 *stage_acc = ctx->m_acc + i * stride;
+        uint32_t *stage_seg = d_seg ? ctx->m_seg + i * stride : nullptr;
+        HIP_TRY(c, hipMemcpyPeerAsync(c->m_acc, c->device, stage_acc, ctx->device, np * sizeof(float4), c->stream));
+        if (d_seg) HIP_TRY(c, hipMemcpyPeerAsync(c->m_seg, c->device, stage_seg, ctx->device, np * 4, c->stream));
+        r = enqueue_render(c, Ri, c->m_acc, d_seg ? c->m_seg : nullptr, c->stream, megakernel, cancel);
+        if (r != OCTPT_OK) {
+            (void)hipStreamSynchronize(c->stream);
+            return r;
+        }
+        HIP_TRY(c, hipMemcpyPeerAsync(stage_acc, ctx->device, c->m_acc, c->device, np * sizeof(float4), c->stream));
+        if (d_seg) HIP_TRY(c, hipMemcpyPeerAsync(stage_seg, ctx->device, c->m_seg, c->device, np * 4, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return OCTPT_OK;
+    });
+    if (st != OCTPT_OK) return st;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, launch_multi_stage(R, n, (uint32_t)stride, d_accum, d_seg, ctx->m_acc, ctx->m_seg, false, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    ctx->kernel_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->launches++;
+    return OCTPT_OK;
+}
+
 void join_inflight(octpt_ctx *ctx) {
     octpt_frame *f = ctx->inflight;
     if (f && f->worker.joinable()) f->worker.join();
@@ -1268,9 +1376,49 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     return OCTPT_OK;
 }
 
+octpt_status octpt_create_multi(const int32_t *devices, uint32_t n, octpt_ctx **out) {
+    if (!out) return OCTPT_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!devices || n == 0 || n > 64) return OCTPT_ERR_INVALID_ARG;
+    if (n == 1) return octpt_create(devices[0], out);
+    try {
+        octpt_ctx *ctx = nullptr;
+        octpt_status st = octpt_create(devices[0], &ctx);  // the first entry's device holds the caller's buffers
+        if (st != OCTPT_OK) return st;
+        for (uint32_t i = 0; i < n && st == OCTPT_OK; ++i) {
+            octpt_ctx *c = nullptr;
+            st = octpt_create(devices[i], &c);
+            if (st == OCTPT_OK) ctx->sub.push_back(c);
+        }
+        if (st != OCTPT_OK) {
+            octpt_destroy(ctx);
+            return st;
+        }
+        // direct peer access between the first device and every other one (xGMI); without it the peer
+        // copies still work, staged by the runtime
+        for (uint32_t i = 1; i < n; ++i) {
+            int a = 0, b = 0;
+            if (devices[i] == devices[0]) continue;
+            if (hipDeviceCanAccessPeer(&a, devices[0], devices[i]) == hipSuccess && a && hipSetDevice(devices[0]) == hipSuccess)
+                (void)hipDeviceEnablePeerAccess(devices[i], 0);
+            if (hipDeviceCanAccessPeer(&b, devices[i], devices[0]) == hipSuccess && b && hipSetDevice(devices[i]) == hipSuccess)
+                (void)hipDeviceEnablePeerAccess(devices[0], 0);
+            (void)hipGetLastError();  // hipErrorPeerAccessAlreadyEnabled for a repeated pair
+        }
+        *out = ctx;
+        return OCTPT_OK;
+    } catch (...) {
+        return OCTPT_ERR_INTERNAL;
+    }
+}
+
+uint32_t octpt_device_entries(const octpt_ctx *ctx) { return !ctx ? 0u : is_multi(ctx) ? (uint32_t)ctx->sub.size() : 1u; }
+
 void octpt_destroy(octpt_ctx *ctx) {
     if (!ctx) return;
     join_inflight(ctx);
+    for (octpt_ctx *c : ctx->sub) octpt_destroy(c);
+    ctx->sub.clear();
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto &e : ctx->pending) {
@@ -1293,6 +1441,8 @@ void octpt_destroy(octpt_ctx *ctx) {
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_subs) (void)hipFree(ctx->d_subs);
     if (ctx->d_beam) (void)hipFree(ctx->d_beam);
+    if (ctx->m_acc) (void)hipFree(ctx->m_acc);
+    if (ctx->m_seg) (void)hipFree(ctx->m_seg);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
     if (ctx->d_lut_float) (void)hipFree(ctx->d_lut_float);
     if (ctx->d_lut_byte) (void)hipFree(ctx->d_lut_byte);
@@ -1306,6 +1456,12 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
     join_inflight(ctx);
     try {
+        if (is_multi(ctx)) {  // a replica on every device entry
+            ctx->has_scene = false;
+            const octpt_status st = for_each_sub(ctx, [&](size_t i) { return octpt_scene_upload(ctx->sub[i], d); });
+            ctx->has_scene = st == OCTPT_OK;
+            return st;
+        }
         std::vector<uint16_t> masks;  // reader-form child masks (C21)
         octpt_status st = validate_scene(ctx, d, masks);
         if (st != OCTPT_OK) return st;
@@ -1394,6 +1550,13 @@ octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *d,
     join_inflight(ctx);
     if (flags & ~OCTPT_BUILD_COMPACT) return fail(ctx, OCTPT_ERR_INVALID_ARG, "unknown build flags");
     try {
+        if (is_multi(ctx)) {  // every device entry builds its own replica
+            ctx->has_scene = false;
+            const octpt_status st =
+                for_each_sub(ctx, [&](size_t i) { return octpt_scene_build_device(ctx->sub[i], d, flags); });
+            ctx->has_scene = st == OCTPT_OK;
+            return st;
+        }
         octpt_status st = validate_head(ctx, d, false);
         if (st != OCTPT_OK) return st;
         if (d->blocks) return fail(ctx, OCTPT_ERR_INVALID_ARG, "a block-value scene is uploaded with its octree");
@@ -1472,6 +1635,10 @@ octpt_status octpt_set_camera(octpt_ctx *ctx, const octpt_camera *c) {
     C.d_factor = 1.0f / tanf(c->fov / 2.0f);         // camera.rs:79
     ctx->C = C;
     ctx->has_camera = true;
+    for (octpt_ctx *sc : ctx->sub) {
+        const octpt_status st = octpt_set_camera(sc, c);
+        if (st != OCTPT_OK) return fail(ctx, st, sc->err);
+    }
     return OCTPT_OK;
 }
 
@@ -1491,6 +1658,9 @@ octpt_status octpt_render_device(octpt_ctx *ctx, const octpt_render_params *p, f
         DevRender R{};
         octpt_status st = make_render(ctx, p, R);
         if (st != OCTPT_OK) return st;
+        if (is_multi(ctx))
+            return multi_render(ctx, *p, R, reinterpret_cast<float4 *>(d_accum), d_seg, static_cast<hipStream_t>(stream),
+                                nullptr);
         return enqueue_render(ctx, R, reinterpret_cast<float4 *>(d_accum), d_seg, static_cast<hipStream_t>(stream),
                               (p->flags & OCTPT_RENDER_MEGAKERNEL) != 0);
     } catch (...) {
@@ -1506,7 +1676,8 @@ void frame_worker(octpt_frame *f, DevRender R, bool megakernel) {
     auto run = [&]() -> octpt_status {
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         HIP_TRY(ctx, hipMemcpyAsync(f->d_accum, f->h_accum, f->n_pixels * 16, hipMemcpyHostToDevice, ctx->stream));
-        octpt_status r = enqueue_render(ctx, R, f->d_accum, nullptr, ctx->stream, megakernel, &f->cancel_requested);
+        octpt_status r = is_multi(ctx) ? multi_render(ctx, f->params, R, f->d_accum, nullptr, ctx->stream, &f->cancel_requested)
+                                       : enqueue_render(ctx, R, f->d_accum, nullptr, ctx->stream, megakernel, &f->cancel_requested);
         if (r != OCTPT_OK) return r;
         if (f->d_rgba) {
             HIP_TRY(ctx, launch_tonemap(f->d_accum, f->d_rgba, (uint32_t)f->n_pixels, ctx->d_lut_byte, ctx->stream));
@@ -1550,6 +1721,7 @@ octpt_status octpt_render_async(octpt_ctx *ctx, const octpt_render_params *p, fl
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         f = new octpt_frame();
         f->ctx = ctx;
+        f->params = *p;
         f->user_accum = accum;
         f->user_rgba = rgba;
         f->n_pixels = accum_pixels(R);
@@ -1650,6 +1822,19 @@ octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *
     if (!ctx->has_scene) return fail(ctx, OCTPT_ERR_INVALID_ARG, "no scene uploaded");
     if (n == 0) return OCTPT_OK;
     if (!rays || !t || !prim) return fail(ctx, OCTPT_ERR_INVALID_ARG, "NULL buffer");
+    if (is_multi(ctx)) {  // one batch on the first entry's replica
+        const octpt_status st = octpt_intersect(ctx->sub[0], rays, last_prim, last_normal, n, t, prim, normal, steps);
+        return st == OCTPT_OK ? st : fail(ctx, st, ctx->sub[0]->err);
+    }
+    // esvo_begin's t_coef = 1 / -|d| comes from rcp_rn, exact for |d| in [2^-23, 2^126] (smaller
+    // components are clamped to 2^-23 first, octree_traversal.rs:86-93): every component finite and
+    // |d| <= 2^126, which any unit direction meets
+    for (size_t i = 0; i < (size_t)n * 6; ++i) {
+        const float v = rays[i];
+        if (!std::isfinite(v) || (i % 6 >= 3 && std::fabs(v) > 0x1p126f))
+            return fail(ctx, OCTPT_ERR_INVALID_ARG,
+                        "ray " + std::to_string(i / 6) + ": origin and direction must be finite, |direction| <= 2^126");
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     float *d_rays = nullptr, *d_ln = nullptr, *d_t = nullptr, *d_n = nullptr;
     uint32_t *d_lp = nullptr, *d_p = nullptr, *d_s = nullptr;
@@ -1689,6 +1874,38 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     if (!cctx || !out) return OCTPT_ERR_INVALID_ARG;
     octpt_ctx *ctx = const_cast<octpt_ctx *>(cctx);
     join_inflight(ctx);
+    if (is_multi(ctx)) {  // the entries' counters summed; kernel_ms = the render calls' wall time
+        octpt_stats tot{};
+        for (octpt_ctx *c : ctx->sub) {
+            octpt_stats cs{};
+            const octpt_status st = octpt_get_stats(c, &cs);
+            if (st != OCTPT_OK) return fail(ctx, st, c->err);
+            tot.paths += cs.paths;
+            tot.segments += cs.segments;
+            tot.esvo_steps += cs.esvo_steps;
+            tot.sphere_tests += cs.sphere_tests;
+            tot.cuboid_tests += cs.cuboid_tests;
+            tot.shade_events += cs.shade_events;
+            tot.texel_reads += cs.texel_reads;
+            tot.extend_launches += cs.extend_launches;
+            tot.shade_launches += cs.shade_launches;
+            tot.extend_ms += cs.extend_ms;
+            tot.shade_ms += cs.shade_ms;
+            tot.build_ms = std::max(tot.build_ms, cs.build_ms);
+            tot.block_tests += cs.block_tests;
+            tot.issued_bytes += cs.issued_bytes;
+            for (int k = 0; k < OCTPT_STAT_COUNT; ++k) tot.drain[k] += cs.drain[k];
+            tot.pool_slots = std::max(tot.pool_slots, cs.pool_slots);
+            tot.chunk_items = std::max(tot.chunk_items, cs.chunk_items);
+            tot.wave_allocs += cs.wave_allocs;
+            tot.beam_restarts += cs.beam_restarts;
+        }
+        tot.build_ms = std::max(tot.build_ms, (double)ctx->build_ms);  // the builder runs on the first device
+        tot.launches = ctx->launches;
+        tot.kernel_ms = ctx->kernel_ms;
+        *out = tot;
+        return OCTPT_OK;
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     for (auto &e : ctx->pending) {
         HIP_TRY(ctx, hipEventSynchronize(e.stop));
@@ -1732,8 +1949,15 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
         }
         std::fprintf(stderr, "\n");
     }
+    // beam-started rays traced again from the cube entry: extend's retraced ones took a
+    // second queue position, which its segment count includes; the drain's restart in place does not
+    unsigned long long redo_main = 0, redo_drain = 0;
+    for (uint32_t r = 0; r < kSegs; ++r) {
+        redo_main += rows[r * kStatRow + kStatBeamRestartWord];
+        redo_drain += rows[(kStatDrainRow + r) * kStatRow + kStatBeamRestartWord];
+    }
     out->paths = v[kStatPaths];
-    out->segments = v[kStatSegments];
+    out->segments = v[kStatSegments] - redo_main;
     out->esvo_steps = v[kStatSteps];
     out->sphere_tests = v[kStatSphereTests];
     out->cuboid_tests = v[kStatCuboidTests];
@@ -1741,6 +1965,7 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     out->texel_reads = v[kStatTexels];
     out->block_tests = v[kStatBlockTests];
     out->issued_bytes = v[kStatIssued];
+    out->beam_restarts = redo_main + redo_drain;
     out->pool_slots = ctx->pool;
     out->chunk_items = ctx->color_cap;
     out->wave_allocs = ctx->wave_allocs_n;
@@ -1757,6 +1982,15 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
 octpt_status octpt_reset_stats(octpt_ctx *ctx) {
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
     join_inflight(ctx);
+    if (is_multi(ctx)) {
+        for (octpt_ctx *c : ctx->sub) {
+            const octpt_status st = octpt_reset_stats(c);
+            if (st != OCTPT_OK) return fail(ctx, st, c->err);
+        }
+        ctx->kernel_ms = 0.0;
+        ctx->launches = 0;
+        return OCTPT_OK;
+    }
     octpt_stats tmp;
     octpt_status st = octpt_get_stats(ctx, &tmp);  // drains pending events
     if (st != OCTPT_OK) return st;

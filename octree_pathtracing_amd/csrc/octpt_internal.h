@@ -209,6 +209,32 @@ static_assert(kStatCount == OCTPT_STAT_COUNT, "octpt_stats::drain order");
 constexpr uint32_t kStatRow = 32;
 constexpr uint32_t kStatWords = 2u * kSegs * kStatRow;
 constexpr uint32_t kStatDrainRow = kSegs;
+// beam-started rays traced again from the cube entry (octpt_stats::beam_restarts): a word of the row
+// past the kStatCount counters, counted by one atomic per event
+constexpr uint32_t kStatBeamRestartWord = 10;
+static_assert(kStatBeamRestartWord >= kStatCount && kStatBeamRestartWord < 12, "below the lane-profile words");
+
+// Multi-device renders (octpt_create_multi): item i of a shard's compact tile order (tile
+// u = i / 64, pixel k = i % 64 of it) is rendered by device entry u % n_dev as its local tile u / n_dev --
+// the entry's own shard of the kernels' tile split, shard_index + (u % n_dev) * shard_count of
+// shard_count * n_dev -- whose compact buffer is staged on the first device at (u % n_dev) * stride.
+// `caller` is the item's index in the caller's buffer (the shard's compact buffer, or the W x H frame);
+// false for a pixel outside the image in a frame layout (never read or written).
+__host__ __device__ inline bool multi_slot(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t shard_index,
+                                           uint32_t shard_count, bool compact, uint32_t n_dev, uint32_t stride,
+                                           uint32_t i, uint32_t &caller, uint32_t &staged) {
+    const uint32_t u = i / 64u, k = i % 64u;
+    staged = (u % n_dev) * stride + (u / n_dev) * 64u + k;
+    if (compact) {
+        caller = i;
+        return true;
+    }
+    const uint32_t t = shard_index + u * shard_count;
+    const uint32_t x = (t % tiles_x) * kTile + k % kTile, y = (t / tiles_x) * kTile + k / kTile;
+    if (x >= W || y >= H) return false;
+    caller = y * W + x;
+    return true;
+}
 
 // kernel launchers (octpt_kernels.hip)
 hipError_t launch_preview(const DevScene &S, const DevCamera &C, const DevRender &R, float4 *accum,
@@ -243,6 +269,10 @@ hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const ui
                           hipStream_t stream);
 hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards,
                           uint32_t stride, float4 *frame, hipStream_t stream);
+// the caller's buffers (accum, and seg when not NULL) <-> the staged compact buffers of n_dev device
+// entries (multi_slot), to_stage = caller -> staging
+hipError_t launch_multi_stage(const DevRender &R, uint32_t n_dev, uint32_t stride, float4 *accum, uint32_t *seg,
+                              float4 *stage_accum, uint32_t *stage_seg, bool to_stage, hipStream_t stream);
 int render_blocks_per_cu(uint32_t depth);
 size_t render_lds_bytes(uint32_t depth);
 

@@ -37,6 +37,10 @@ namespace {
 #define MAT_FLAG_REFRACTIVE 0x4u
 #define MAT_FLAG_SUBSURFACE 0x2u  // MaterialFlags::SUBSURFACE_SCATTER (material.rs:9)
 #define MAX_PATH_SEGMENTS 64u  // [C15] next_intersection calls per path (grazing self-hit loops)
+// a beam start carries, in its low mantissa bits, a bound of the reference iterations it skips (beam_kernel)
+constexpr uint32_t kBeamIterBits = 10u;
+constexpr uint32_t kBeamIterMask = (1u << kBeamIterBits) - 1u;
+static_assert(OCTREE_MAX_STEPS <= kBeamIterMask + 1u, "the skipped-iteration bound fits its bits");
 
 // ---------------------------------------------------------------------------
 // f32 vector helpers (glam Vec3A operation order, see oracle/cpu_ref.c)
@@ -226,10 +230,20 @@ struct Esvo {
     uint32_t parent, pmask, idx, mirror, iter;  // scale = exponent of scale_exp2 + OCTREE_MAX_SCALE - 127
 };
 
+// E.iter: the low 16 bits are the iteration count the reference's cap applies to (OCTREE_MAX_STEPS,
+// octree_traversal.rs:127); the high 16 bits are the iteration bound a beam start begins the count at
+// (esvo_begin, beam_kernel), 0 for every other ray.  Executed iterations = low - high.
+__device__ __forceinline__ bool esvo_capped(uint32_t it) { return (uint16_t)it >= (uint16_t)OCTREE_MAX_STEPS; }
+__device__ __forceinline__ uint32_t esvo_executed(uint32_t it) { return (it & 0xFFFFu) - (it >> 16); }
+// a beam-started ray that reached the cap: the reference may still have had iterations left (the bound
+// over-counts the ones the beam skipped), so the ray is traced again from its cube entry
+__device__ __forceinline__ bool esvo_beam_capped(uint32_t it) { return (it >> 16) != 0u && esvo_capped(it); }
+
 struct Counters {
     uint32_t paths, segs, steps, sph, cub, shade, tex;
     uint32_t blk;  // block-value leaf tests (C23)
     uint32_t ib;   // issued load bytes of extend (OCTPT_COUNT_ISSUED builds; see ISSUED below)
+    uint32_t redo;  // beam-started rays traced again from the cube entry (esvo_beam_capped; stat word kStatBeamRestartWord)
 #ifdef OCTPT_PROFILE_LANES  // diagnostic builds: per-wave lane occupancy of extend's step (stat words 8..)
     uint32_t p_iters, p_active, p_leaf_it, p_leaf_ln, p_pop_it, p_pop_ln, p_push_it, p_desc_ln, p_exact, p_fold_it,
         p_fold_ln, p_dfold_it, p_dfold_ln;
@@ -754,12 +768,40 @@ __device__ __forceinline__ TraceRay make_trace_ray(const DevScene &S, v3 o, v3 d
     return t;
 }
 
+// The cell of the root that ESVO's first iteration processes: the child holding the point at t_min
+// (octree_traversal.rs:113-125).
+__device__ __forceinline__ void esvo_first_child(Esvo &E) {
+    E.idx = 0u;
+    E.pos = V(1.0f, 1.0f, 1.0f);
+    const v3 upper = vsub(vscale(E.t_coef, 1.5f), E.t_bias);
+    if (upper.x > E.t_min) { E.idx ^= 1u; E.pos.x = 1.5f; }
+    if (upper.y > E.t_min) { E.idx ^= 2u; E.pos.y = 1.5f; }
+    if (upper.z > E.t_min) { E.idx ^= 4u; E.pos.z = 1.5f; }
+}
+
+// ESVO's state at the cube entry from the ray's t_coef / t_bias / mirror (octree_traversal.rs:79-112; the
+// first child follows, esvo_first_child): the walk of the reference from its first iteration.  Also how a
+// beam-started ray that reached the step cap starts again (esvo_beam_capped): its t_coef, t_bias and
+// mirror are the ray's own, only the walk restarts.
+__device__ __forceinline__ void esvo_root(const DevScene &S, Esvo &E) {
+    E.parent = S.root;
+    E.pmask = S.root_mask;
+    E.scale_exp2 = 0.5f;
+    E.t_min = tmx(tmax3(vsub(vscale(E.t_coef, 2.0f), E.t_bias)), 0.0f);
+    E.t_max = tmin3(vsub(E.t_coef, E.t_bias));
+    E.h = E.t_max;
+    E.iter = 0u;
+}
+
 // t_start > 0 (a camera ray with a beam start, beam_kernel): no octree leaf lies within the ray's
 // tile frustum before t_start, so ESVO starts there instead of at the cube entry (Laine & Karras'
 // beam optimisation).  ESVO lands in the cell that holds the point at t_start and walks on from it;
 // the cells it skips are empty, so the first leaf it meets, and with it the hit, is the reference's.
 // t_start less a bound of ESVO's own rounding of t-values (which grows with |t_coef|, i.e. for
-// rays near-parallel to an axis), clamped to the cube exit.
+// rays near-parallel to an axis), clamped to the cube exit.  The low kBeamIterBits of t_start's bits
+// hold a bound of the reference iterations before the start (beam_kernel), at which the iteration
+// count begins, so that the reference's step cap still applies (a ray reaching it is traced again from
+// its cube entry, esvo_beam_capped).
 template <uint32_t kS>
 __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk,
                                   float t_start = 0.0f) {
@@ -771,9 +813,6 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     v3 ro = vscale(ray.o, osc);
     v3 rd = ray.d;
     ro = vadd(ro, V(1.0f, 1.0f, 1.0f));
-    E.parent = S.root;
-    E.pmask = S.root_mask;
-    E.scale_exp2 = 0.5f;
     const uint32_t epsb = __float_as_uint(OCTREE_EPSILON) & 0x7FFFFFFFu;
     if (fabsf(rd.x) < OCTREE_EPSILON) rd.x = __uint_as_float(epsb | (__float_as_uint(rd.x) & 0x80000000u));
     if (fabsf(rd.y) < OCTREE_EPSILON) rd.y = __uint_as_float(epsb | (__float_as_uint(rd.y) & 0x80000000u));
@@ -790,22 +829,18 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
     if (rd.x > 0.0f) { E.mirror |= 1u; E.t_bias.x = 3.0f * E.t_coef.x - E.t_bias.x; }
     if (rd.y > 0.0f) { E.mirror |= 2u; E.t_bias.y = 3.0f * E.t_coef.y - E.t_bias.y; }
     if (rd.z > 0.0f) { E.mirror |= 4u; E.t_bias.z = 3.0f * E.t_coef.z - E.t_bias.z; }
-    E.t_min = tmx(tmax3(vsub(vscale(E.t_coef, 2.0f), E.t_bias)), 0.0f);
-    E.t_max = tmin3(vsub(E.t_coef, E.t_bias));
+    esvo_root(S, E);
     if (t_start > 0.0f) {
         const float ro_m = tmx(tmx(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z));
         const float tc_m = -tmn(tmn(E.t_coef.x, E.t_coef.y), E.t_coef.z);
         const float margin = 0x1p-16f * (4.0f + ro_m) * tc_m;
         E.t_min = tmx(E.t_min, tmn(t_start - margin, E.t_max));
+        // the reference's step cap counts from the cube entry: the count starts at beam_kernel's bound
+        // of the iterations skipped (carried in t_start's low mantissa bits, beam_pack)
+        const uint32_t skipped = __float_as_uint(t_start) & kBeamIterMask;
+        E.iter = skipped | (skipped << 16);
     }
-    E.h = E.t_max;
-    E.idx = 0u;
-    E.pos = V(1.0f, 1.0f, 1.0f);
-    const v3 upper = vsub(vscale(E.t_coef, 1.5f), E.t_bias);
-    if (upper.x > E.t_min) { E.idx ^= 1u; E.pos.x = 1.5f; }
-    if (upper.y > E.t_min) { E.idx ^= 2u; E.pos.y = 1.5f; }
-    if (upper.z > E.t_min) { E.idx ^= 4u; E.pos.z = 1.5f; }
-    E.iter = 0u;
+    esvo_first_child(E);
 }
 
 enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
@@ -959,7 +994,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
                                 uint32_t &prim, PrimHit &h) {
     // :128-130: max_dst = 1024 * 2^-depth > 0, so the reference's `max_dst >= 0` guard always holds
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
-    const bool stopped = (E.iter >= OCTREE_MAX_STEPS) | (E.t_min > max_dst);
+    const bool stopped = esvo_capped(E.iter) | (E.t_min > max_dst);
     E.iter += stopped ? 0u : 1u;
     const v3 t_corner = vsub(vmul(E.pos, E.t_coef), E.t_bias);
     const float tc_max = tmin3(t_corner);
@@ -1044,7 +1079,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const v3 tc2 = vsub(vmul(E.pos, E.t_coef), E.t_bias);
         const float tc2_max = tmin3(tc2);
         const float tv2_max = tmn(E.t_max, tc2_max);
-        const bool d2 = (((E.pmask >> cidx2) & 0x101u) == 0x001u) & (E.iter < OCTREE_MAX_STEPS) &
+        const bool d2 = (((E.pmask >> cidx2) & 0x101u) == 0x001u) & !esvo_capped(E.iter) &
                         !(E.t_min > max_dst) & (E.t_min <= tv2_max);
 #ifdef OCTPT_PROFILE_LANES
         prof_wave(cnt.p_dfold_it, cnt.p_dfold_ln, d2);
@@ -1067,7 +1102,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
 #pragma unroll
     for (int k = 0; k < kFolds; ++k) {  // kFolds folds at most per step
     const bool fold = !leaf_hit & !stopped & !pop & (((E.pmask >> (E.idx ^ E.mirror)) & 1u) == 0u) &
-                      (E.iter < OCTREE_MAX_STEPS) & !(E.t_min > max_dst);
+                      !esvo_capped(E.iter) & !(E.t_min > max_dst);
 #ifdef OCTPT_PROFILE_LANES
     prof_wave(cnt.p_fold_it, cnt.p_fold_ln, fold);
 #endif
@@ -1531,6 +1566,8 @@ __device__ inline void flush_counters(const Counters &cnt, unsigned long long *s
         if ((threadIdx.x & 63u) == 0u && s)
             atomicAdd(&stats[(row_base + blockIdx.x % kSegs) * kStatRow + i], s);
     }
+    const unsigned long long r = wave_sum(cnt.redo);
+    if ((threadIdx.x & 63u) == 0u && r) atomicAdd(&stats[(row_base + blockIdx.x % kSegs) * kStatRow + kStatBeamRestartWord], r);
 }
 
 // wave-aggregated atomic ticket: each lane with `want` gets a distinct value from *ctr
@@ -1736,6 +1773,9 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
 //   pa[slot]   = (T.xyz, L.x)  pb[slot] = (L.y, L.z, rng, item)  pc[slot] = (cur_mat, depth | spec<<8 | segs<<16)
 //   a camera ray with a beam start: ray1 bit 30 set, ray0.w = the start t (its last_prim is kPrimNone)
 constexpr uint32_t kRayBeamBit = 0x40000000u;  // slots < 2^30 (the pool cap)
+// a miss record's second word for a beam-started ray that reached the reference's step cap: shade queues
+// the same ray again without its beam start (the walk from the cube entry), no segment counted
+constexpr uint32_t kHitRetrace = 1u;
 __device__ __forceinline__ void store_ray(const WaveBuffers &B, uint32_t q, uint32_t pos, uint32_t slot,
                                           const PathState &ps) {
     const bool beam = ps.beam > 0.0f && ps.path_segs == 1u;
@@ -2071,13 +2111,16 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                     // sphere instance, whose allocation is better off as it is: C3 -1 % with it)
                     uint32_t p = pos;
                     if constexpr (kPrims != kPrimsSpheres) asm volatile("" : "+v"(p));
+                    // a miss: (kPrimNone, 0), or (kPrimNone, kHitRetrace) for a beam-started ray that reached
+                    // the step cap, which shade queues again without its beam start (esvo_beam_capped)
+                    const uint2 miss = make_uint2(kPrimNone, esvo_beam_capped(E.iter) ? kHitRetrace : 0u);
                     if constexpr (kPrims == kPrimsBlocks) {  // (face << 27 | block or the quad, t) + (u, v) (C23)
-                        B.hit[p] = rs == kStepHit ? make_uint2(prim, __float_as_uint(h.t)) : make_uint2(kPrimNone, 0u);
+                        B.hit[p] = rs == kStepHit ? make_uint2(prim, __float_as_uint(h.t)) : miss;
                         if (rs == kStepHit) B.huv[p] = make_float2(h.u, h.v);
                     } else {
-                        B.hit[p] = rs == kStepHit ? hit_record(prim, h) : make_uint2(kPrimNone, 0u);
+                        B.hit[p] = rs == kStepHit ? hit_record(prim, h) : miss;
                     }
-                    cnt.steps += E.iter;
+                    cnt.steps += esvo_executed(E.iter);
                     active = false;
                 }
             }
@@ -2111,9 +2154,19 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     } else {
         load_path(B, slot, r0, r1, ps, item);
     }
+    const uint2 hr = *hit_rec;
+    if (__builtin_expect((hr.x == kPrimNone) & (hr.y == kHitRetrace), 0)) {
+        // a beam-started camera ray that reached the reference's step cap (extend, esvo_beam_capped): the
+        // same ray is queued again without its beam start, for the walk from the cube entry.  No segment
+        // is counted; the path state is the seed's (stored now when this shade rebuilt it from the item).
+        if (first) store_path(B, slot, ps, item);
+        ps.n = V(0.0f, 0.0f, 0.0f);
+        ps.beam = 0.0f;
+        cnt.redo++;
+        return true;
+    }
     const bool was_shadow = kNee && ps.shadow;
     if (was_shadow) load_nee(B, slot, ps);
-    const uint2 hr = *hit_rec;
     const bool hit = hr.x != kPrimNone;
     if (hit && S.has_blocks) {  // block-value leaf (C23): the record's (u, v) beside it
         const float2 uv = *huv_rec;
@@ -2253,10 +2306,16 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                 uint32_t prim = kPrimNone;
                 PrimHit h;
                 int rs;
-                do {
-                    rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
-                } while (rs == kStepContinue);
-                cnt.steps += E.iter;
+                for (;;) {
+                    do {
+                        rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
+                    } while (rs == kStepContinue);
+                    cnt.steps += esvo_executed(E.iter);
+                    if (!((rs == kStepMiss) & esvo_beam_capped(E.iter))) break;
+                    cnt.redo++;  // traced again from the cube entry, in place (shade_lane's retrace, inline)
+                    esvo_root(S, E);
+                    esvo_first_child(E);
+                }
                 cnt.segs++;
                 uint2 hr;
                 if constexpr (kPrims == kPrimsBlocks)
@@ -2386,6 +2445,23 @@ constexpr uint32_t kBeamVisits = OCTPT_BEAM_VISITS;  // cells visited per tile; 
 #define OCTPT_BEAM_LOD 0.0f
 #endif
 constexpr float kBeamLod = OCTPT_BEAM_LOD;
+
+// A tile's start t with, in its low kBeamIterBits bits, a bound of the reference iterations a ray of the
+// tile runs before it (t is rounded down first, so the packed value never exceeds it).  The reference
+// walk (octree_traversal.rs:127-300) spends one iteration per child cell it processes -- a descend
+// enters the cell, an advance leaves it, and a cell left by a pop is never processed again -- and it
+// processes at most 4 children of an octant it enters, since in mirrored coordinates each axis can
+// step across the octant's midplane once.  Every octant a ray of the tile enters before t meets the
+// pyramid nearer than t, so this walk entered it too (it prunes only by the pyramid and by distances
+// >= the final start): 4 * nodes bounds those iterations.  E.iter starts there (esvo_begin); a bound at
+// or past the cap (OCTREE_MAX_STEPS) gives no start (0), as does a start too small to carry it.
+__device__ __forceinline__ float beam_pack(float t, uint32_t nodes) {
+    const uint32_t bound = 4u * nodes;
+    const uint32_t b = __float_as_uint(t);
+    if (bound >= OCTREE_MAX_STEPS || b < 2u * (kBeamIterMask + 1u)) return 0.0f;
+    return __uint_as_float(((b - (kBeamIterMask + 1u)) & ~kBeamIterMask) | bound);
+}
+
 __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRender R, uint32_t n_tiles,
                                                   float *__restrict__ beam) {
     // thread i: beam tile i % kBeamSub of the shard's render tile i / kBeamSub (item_pixel's tile order),
@@ -2450,6 +2526,7 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
         return pm;
     };
     bool exhausted = S.depth >= (uint32_t)kBeamLevels;
+    uint32_t nodes = 1u;  // octants the walk entered (the root included)
     if (!exhausted && box(V(1.0f, 1.0f, 1.0f), 1.0f) >= 0.0f) {
         int lv = 0;
         st_base[0][t] = S.root;
@@ -2472,6 +2549,7 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
             if (kind == 0x101u || lv + 1 >= kBeamLevels || h <= lod * d) { best = d; continue; }  // leaf / small cell
             const uint2 slot = S.node_child[st_base[lv][t] + __popc(m & ((1u << ci) - 1u))];
             ++lv;
+            ++nodes;
             st_base[lv][t] = slot.x;
             st_mask[lv][t] = slot.y;
             st_rem[lv][t] = order(slot.y);
@@ -2480,7 +2558,7 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
             st_lz[lv][t] = lo.z;
         }
     }
-    beam[tile] = exhausted ? 0.0f : best * (1.0f - 0x1p-16f);
+    beam[tile] = exhausted ? 0.0f : beam_pack(best * (1.0f - 0x1p-16f), nodes);
 }
 
 __global__ void tonemap_kernel(const float4 *__restrict__ accum, uchar4 *__restrict__ out, uint32_t n,
@@ -2502,6 +2580,23 @@ __global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t N, const float4 
     const uint32_t t = (y / kTile) * tiles_x + x / kTile;
     const uint32_t shard = t % N, lt = t / N;
     frame[i] = shards[(size_t)shard * stride + (size_t)lt * 64u + (y % kTile) * kTile + (x % kTile)];
+}
+
+// a multi-device render's scatter (to_stage) / gather of the caller's buffers (multi_slot)
+__global__ void multi_stage_kernel(DevRender R, uint32_t n_dev, uint32_t stride, float4 *__restrict__ accum,
+                                   uint32_t *__restrict__ seg, float4 *__restrict__ stage_accum,
+                                   uint32_t *__restrict__ stage_seg, uint32_t to_stage) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R.total_items) return;
+    uint32_t c, st;
+    if (!multi_slot(R.W, R.H, R.tiles_x, R.shard_index, R.shard_count, R.compact != 0u, n_dev, stride, i, c, st)) return;
+    if (to_stage) {
+        stage_accum[st] = accum[c];
+        if (seg) stage_seg[st] = seg[c];
+    } else {
+        accum[c] = stage_accum[st];
+        if (seg) seg[c] = stage_seg[st];
+    }
 }
 
 }  // namespace
@@ -2655,6 +2750,13 @@ hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R
 
 hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const uint8_t *lut_byte, hipStream_t stream) {
     hipLaunchKernelGGL(tonemap_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, accum, out, n, lut_byte);
+    return hipGetLastError();
+}
+
+hipError_t launch_multi_stage(const DevRender &R, uint32_t n_dev, uint32_t stride, float4 *accum, uint32_t *seg,
+                              float4 *stage_accum, uint32_t *stage_seg, bool to_stage, hipStream_t stream) {
+    hipLaunchKernelGGL(multi_stage_kernel, dim3((R.total_items + 255u) / 256u), dim3(256), 0, stream, R, n_dev, stride,
+                       accum, seg, stage_accum, stage_seg, to_stage ? 1u : 0u);
     return hipGetLastError();
 }
 

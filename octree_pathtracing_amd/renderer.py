@@ -80,17 +80,25 @@ class FrameInFlight:
 
 
 class HipRenderer:
-    """RenderingBackend implemented on one MI355X (HIP device `device`)."""
+    """RenderingBackend implemented on one MI355X (HIP device `device`), or on several GPUs of the node
+    through one context (`devices`: a list of HIP device ids, octpt_create_multi; ids may repeat)."""
 
     def __init__(self, device: int = 0, resolution=(500, 500), target_spp: int = 1, seed: int = 1,
-                 max_depth: int = 5, lib_path=None):
+                 max_depth: int = 5, lib_path=None, devices=None):
         # lib_path: another build of the same ABI (bench.py's issued-bytes diagnostic library)
         self._lib = _lib.load(lib_path) if lib_path else _lib.load()
         ctx = C.c_void_p()
-        st = self._lib.octpt_create(int(device), C.byref(ctx))
+        if devices is None:
+            st = self._lib.octpt_create(int(device), C.byref(ctx))
+            what = f"octpt_create(device={device})"
+        else:
+            devs = (C.c_int32 * len(devices))(*map(int, devices))
+            st = self._lib.octpt_create_multi(devs, len(devices), C.byref(ctx))
+            what = f"octpt_create_multi(devices={list(devices)})"
         if st != _lib.OK:
-            raise _lib.OctptError(st, f"octpt_create(device={device}) failed: no usable gfx950 device")
+            raise _lib.OctptError(st, f"{what} failed: no usable gfx950 device")
         self._ctx = ctx
+        self.device_entries = int(self._lib.octpt_device_entries(ctx))
         self._camera = Camera()
         self._resolution = tuple(resolution)
         self._mode = RendererMode.PathTraced

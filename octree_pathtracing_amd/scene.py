@@ -799,7 +799,26 @@ def random_cuboids(seed: int, n: int, world: float, emin: float, emax: float):
 
 
 CONFIGS = ("C1", "C1-as-is", "C2", "C3", "C4", "C5", "tiny", "blocks", "C3-in", "C5-fp", "C5b", "C5b-fp", "blocks-b",
-           "C5s", "C5s-fp", "C5s-small")
+           "C5s", "C5s-fp", "C5s-small", "cap")
+
+
+def step_cap_world(scene: Scene, seed: int, floor_len: int = 1024, floor_w: int = 64, wall_x: int = 600):
+    """A block-value world whose near-horizontal camera rays reach the reference's ESVO step
+    cap (OCTREE_MAX_STEPS = 1000, octree_traversal.rs:13, 127) and miss: a checkerboard floor of blocks at
+    y = 0 (every level-1 octant along the floor is present, so a ray skimming over it at 1 < y < 2 spends
+    ~2 iterations per unit of distance without meeting a leaf) and a stone wall at x = wall_x that only a
+    walk counting fewer iterations than the reference would reach.  Sets scene.blocks / cells."""
+    mat = block_materials(scene, seed)
+    scene.blocks = np.array([[mat["grass_side"]] * 2 + [mat["dirt"], mat["grass_top"]] + [mat["grass_side"]] * 2,
+                             [mat["stone"]] * 6], np.uint32)
+    scene.block_model = np.full(2, _lib.MODEL_NONE, np.uint32)
+    xx, zz = np.meshgrid(np.arange(floor_len), np.arange(floor_w), indexing="ij")
+    keep = ((xx + zz) % 2 == 0) & ((xx < wall_x) | (xx >= wall_x + 4))
+    floor = np.stack([xx[keep], np.zeros(keep.sum(), np.int64), zz[keep], np.zeros(keep.sum(), np.int64)], 1)
+    wx, wy, wz = np.meshgrid(np.arange(wall_x, wall_x + 4), np.arange(8), np.arange(floor_w), indexing="ij")
+    wall = np.stack([wx.ravel(), wy.ravel(), wz.ravel(), np.ones(wx.size, np.int64)], 1)
+    scene.cells = np.concatenate([floor, wall]).astype(np.uint32)
+    return scene
 
 
 C5_SIDE = 1000  # columns per side: 1,001,225 unit blocks with the exposed-side fill
@@ -833,6 +852,18 @@ def make_config(name: str, *, seed: int = 1, build: bool = True):
             sc.build_octree(depth)
         else:
             sc._depth = depth  # type: ignore[attr-defined]
+        return sc, cam, rs
+    if name == "cap":
+        # camera rays that reach the reference's step cap (the beam start's iteration bound):
+        # a wide, 8-row image at the horizon over step_cap_world's floor
+        sc = Scene()
+        step_cap_world(sc, seed)
+        cam = Camera(eye=(-20.0, 1.5, 31.7), direction=(1.0, 0.0, 0.0), up=(0.0, 1.0, 0.0))
+        rs = RenderSettings(4096, 8, 1, max_depth=2, seed=seed)
+        if build:
+            sc.build_octree(10)
+        else:
+            sc._depth = 10  # type: ignore[attr-defined]
         return sc, cam, rs
     sc = Scene()
     if name in ("C1", "C1-as-is"):

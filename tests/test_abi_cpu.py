@@ -75,7 +75,7 @@ def test_reference_layout_sizes():
 
 
 def test_version_and_devices(lib):
-    assert lib.octpt_abi_version() == _lib.OCTPT_ABI_VERSION == 3
+    assert lib.octpt_abi_version() == _lib.OCTPT_ABI_VERSION == 4
     assert lib.octpt_device_count() >= 0
 
 

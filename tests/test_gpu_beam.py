@@ -141,3 +141,105 @@ def test_rcp_exhaustive(torch_cuda):
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "mismatches 0" in p.stdout, p.stdout
+
+
+def assert_parity_shipped(gpu, ref, tag):
+    """test_gpu_parity.assert_parity for the shipped default (beam on): everything exact but the ESVO
+    iteration total, which is at most the oracle's (the beam skips iterations over empty cells)."""
+    from tests.test_gpu_parity import REL_TOL_FORWARD, rel_err
+
+    acc, segs, st = gpu
+    racc, rsegs, rst = ref
+    assert np.array_equal(segs, rsegs), f"{tag}: per-pixel segment counts differ at {np.argwhere(segs != rsegs)[:5]}"
+    assert st["segments"] == rst["segments"], tag
+    assert st["esvo_steps"] <= rst["esvo_steps"], (tag, st["esvo_steps"], rst["esvo_steps"])
+    # a camera ray whose beam start reached the step cap is traced again from the cube entry (beam_restarts):
+    # the leaf tests of its first walk are work done on top of the reference's
+    tests, ref_tests = st["sphere_tests"] + st["cuboid_tests"], rst["prim_tests"]
+    blocks, ref_blocks = st.get("block_tests", 0), rst.get("block_tests", 0)
+    if st["beam_restarts"] == 0:
+        assert tests == ref_tests and blocks == ref_blocks, tag
+    else:
+        assert tests >= ref_tests and blocks >= ref_blocks, tag
+    assert st["shade_events"] == rst["shade_events"], tag
+    assert np.all(np.isfinite(acc)), tag
+    e = rel_err(acc, racc)
+    assert e.max() <= REL_TOL_FORWARD, f"{tag}: max rel err {e.max()} at {np.unravel_index(e.argmax(), e.shape)}"
+    return float((acc == racc).mean())
+
+
+@pytest.mark.parametrize("name,spp", [("C3", 2), ("C4", 1), ("C5", 1), ("C5b", 1)])
+def test_beam_fullframe_oracle(torch_cuda, beam, name, spp):
+    """The shipped default (the camera rays' beam start on, 4x4 beam tiles) against the oracle over WHOLE
+    BASELINE-size frames (C3 1920x1080, C4 / C5 / C5b 3840x2160): the beam table's indexing at these tile
+    counts and every beam start enter the comparison, not only beam == no-beam at reduced sizes."""
+    from octree_pathtracing_amd import scene as S
+    from tests.test_gpu_parity import oracle
+
+    sc, cam, rs = S.make_config(name)
+    assert (rs.width, rs.height) == ((1920, 1080) if name == "C3" else (3840, 2160))
+    rs.spp = spp
+    gpu = gpu_render(torch_cuda, beam, sc, cam, rs)
+    assert gpu[2]["paths"] == rs.width * rs.height * spp
+    ref = oracle(sc, cam, rs, forward=True, threads=16)
+    exact = assert_parity_shipped(gpu, ref, name)
+    assert exact > 0.999, f"{name}: only {exact:.4%} of channels bit-identical"
+    assert gpu[2]["esvo_steps"] < ref[2]["esvo_steps"], name  # the beam did skip iterations
+
+
+@pytest.mark.parametrize("name", ["C3", "C5b"])
+def test_beam_near_axis_fullframe(torch_cuda, renderer, beam, name):
+    """A camera looking straight down an axis, so that the rays near the image centre are near-parallel to
+    the other two: their t_coef = 1 / -|d| is large and esvo_begin's rounding margin for the beam start,
+    2^-16 (4 + max|ro|) max|t_coef|, is at its widest.  Whole 1080p frames, beam on against the oracle (and
+    beam off exactly, iteration total included)."""
+    from octree_pathtracing_amd import scene as S
+    from tests.test_gpu_parity import assert_parity, oracle
+
+    sc, _, rs = S.make_config(name)
+    if name == "C3":  # along +z from outside the cube, through the sphere cloud
+        cam = S.Camera(eye=(128.37, 131.21, -40.0), direction=(0.0, 0.0, 1.0), up=(0.0, 1.0, 0.0))
+    else:  # straight down onto the voxel terrain from above it
+        cam = S.Camera(eye=(517.3, 300.0, 533.9), direction=(0.0, -1.0, 0.0), up=(0.0, 0.0, 1.0))
+    rs.width, rs.height, rs.spp = 1920, 1080, 1
+    ref = oracle(sc, cam, rs, forward=True, threads=16)
+    on = gpu_render(torch_cuda, beam, sc, cam, rs)
+    assert_parity_shipped(on, ref, name + " beam")
+    assert on[2]["esvo_steps"] < ref[2]["esvo_steps"], name
+    off = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    assert_parity(off, ref, name + " no beam")
+
+
+def test_beam_step_cap(torch_cuda, renderer, beam):
+    """The reference's step cap (OCTREE_MAX_STEPS = 1000, octree_traversal.rs:127): near-horizontal camera
+    rays over step_cap_world's floor run out of iterations and miss, in the oracle, before the wall that a
+    walk counting only the iterations after the beam start would reach.  The beam start carries a bound of
+    the iterations it skips (beam_kernel), the count starts there, and a ray reaching the cap is traced
+    again from its cube entry (esvo_beam_capped; shade's retrace): beam on == oracle, with restarts."""
+    from octree_pathtracing_amd import scene as S
+    from oracle import cpu_ref
+    from tests.test_gpu_parity import assert_parity, oracle
+
+    sc, cam, rs = S.make_config("cap")
+    ref = oracle(sc, cam, rs, forward=True)
+    # the fixture does what it is for: camera rays of the oracle walk end on the cap
+    W, H = rs.width, rs.height
+    d = 1.0 / np.tan(cam.fov / 2)
+    D, U = np.array(cam.direction), np.array(cam.up)
+    R = np.cross(D, U)
+    ys, xs = np.mgrid[0:H, 0:W]
+    v = (d * D[None, None] + (((2 * xs + 1) - W) / W)[..., None] * R + (((2 * (H - ys) - 1) - H) / W)[..., None] * U)
+    v /= np.linalg.norm(v, axis=-1, keepdims=True)
+    rays = np.concatenate([np.broadcast_to(np.array(cam.eye), v.shape), v], -1).reshape(-1, 6)
+    steps = cpu_ref.intersect(sc, rays.astype(np.float32))[3]
+    assert (steps >= 1000).sum() > 1000, "the fixture's camera rays must reach the step cap"
+    on = gpu_render(torch_cuda, beam, sc, cam, rs)
+    assert_parity_shipped(on, ref, "cap beam")
+    assert on[2]["beam_restarts"] > 0, "no beam-started ray reached the cap: the restart is untested"
+    off = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    assert_parity(off, ref, "cap no beam")
+    assert off[2]["beam_restarts"] == 0
+    small = gpu_render(torch_cuda, beam_pool_small := _renderer_with({"OCTPT_BEAM": "1", "OCTPT_POOL": "4096",
+                                                                       "OCTPT_CHUNK": "8192"}), sc, cam, rs)
+    beam_pool_small.close()
+    assert_parity_shipped(small, ref, "cap beam, small pool (regenerated camera rays)")
