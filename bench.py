@@ -420,13 +420,15 @@ def main():
     }
     if multi:
         out["config"]["capi_devices"] = multi
-    if world > 1 and not args.no_capi_multi and args.dist_backend == "nccl":
+    if world > 1 and not args.no_capi_multi:
         # the same frame through the C-ABI path a Rust host calls: one process (rank 0), one multi-device
-        # context over the N devices, tiles gathered inside liboctpt; the other ranks wait
+        # context over the N devices, tiles gathered inside liboctpt; the other ranks wait.
+        # (gloo rehearsals of N ranks on fewer GPUs repeat device ids, as the ranks do)
         dist.barrier()
         if rank == 0:
             try:
-                out["capi_multi"] = capi_multi_measure(sc, cam, rs, list(range(world)), args.steps, args.warmup)
+                devs = [i % max(n_dev, 1) for i in range(world)]
+                out["capi_multi"] = capi_multi_measure(sc, cam, rs, devs, args.steps, args.warmup)
             except Exception as e:  # reported, never fatal to the bench line
                 out["capi_multi"] = {"error": f"{type(e).__name__}: {e}"}
         dist.barrier()

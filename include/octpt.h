@@ -254,6 +254,9 @@ typedef struct octpt_stats {
     /* camera rays whose beam start reached the reference's step cap and were traced again from the
      * cube entry (their iterations before the restart are in esvo_steps too) */
     uint64_t beam_restarts;
+    /* hit records a field of which the path that produced the hit left unwritten: counted only by the
+     * OCTPT_CHECK_HITS diagnostic build of the library, else 0 */
+    uint64_t hit_check_failures;
 } octpt_stats;
 
 /* --- library / context ------------------------------------------------------ */

@@ -175,7 +175,8 @@ class Stats(C.Structure):
                 ("extend_launches", C.c_uint64), ("shade_launches", C.c_uint64), ("extend_ms", C.c_double),
                 ("shade_ms", C.c_double), ("build_ms", C.c_double), ("block_tests", C.c_uint64),
                 ("issued_bytes", C.c_uint64), ("drain", C.c_uint64 * STAT_COUNT), ("pool_slots", C.c_uint64),
-                ("chunk_items", C.c_uint64), ("wave_allocs", C.c_uint64), ("beam_restarts", C.c_uint64)]
+                ("chunk_items", C.c_uint64), ("wave_allocs", C.c_uint64), ("beam_restarts", C.c_uint64),
+                ("hit_check_failures", C.c_uint64)]
 
     def as_dict(self) -> dict:
         d = {name: getattr(self, name) for name, _ in self._fields_}

@@ -100,7 +100,9 @@ struct octpt_ctx {
     BuildScratch build_scratch;
     int blocks_per_cu_cache[kMaxDepth + 1] = {0};
     int extend_bpc_cache[kMaxDepth + 1][4] = {};  // [depth][kPrims]
-    int shade_bpc_cache[2][2][2] = {};            // [sun sampling][LDS tables][regeneration]
+    int shade_bpc_cache[2][2][3] = {};            // [sun sampling][LDS tables][shade_mode]
+    bool lean_scene = false;  // no emitters, no sun sampling: the lean path state applies when the pool holds the chunk
+    bool no_lean = false;     // OCTPT_LEAN=0: always the 40-B path state (A/B, tests)
     // wavefront pool (grown on demand)
     WaveBuffers wb{};
     size_t pool = 0, color_cap = 0, nee_pool = 0;  // nee_pool: slots of the sun-sampling planes (wb.pd)
@@ -572,6 +574,13 @@ octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_
     make_sun(d->sun, lf, S.sun);
     S.sun.f_sub_surface = d->f_sub_surface;
     S.emitters = d->emitters_enabled ? 1 : 0;
+    // the lean path state (WaveBuffers::lean): a continuing path's radiance is 0 when nothing adds light
+    // before its end -- no emitting material (shade_segment adds emittance > EPSILON when emitters are on)
+    // and no sun sampling (C18 adds the sun's direct light mid-path)
+    bool emissive = false;
+    for (uint32_t i = 0; i < d->material_count && d->emitters_enabled; ++i)
+        emissive = emissive || d->materials[i].emittance > 5e-8f;  // RAY_EPSILON
+    ctx->lean_scene = !emissive && !d->sun.sun_sampling;
     return OCTPT_OK;
 }
 
@@ -917,11 +926,11 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const int seg_blocks = (int)(kSegs * 64u / kBlock);
     // blocks per CU: what the instance's registers allow (4 with regeneration, 5 without), or OCTPT_SHADE_BPC
     const uint32_t shade_bpc_env = std::min<uint32_t>(env_u32("OCTPT_SHADE_BPC", 0u), 8u);
-    auto grid_shade_of = [&](bool regen) {
+    auto grid_shade_of = [&](int mode) {
         int &cached = ctx->shade_bpc_cache[ctx->S.sun.sun_sampling ? 1 : 0]
                                           [shade_lds_tables(ctx->S) ? 1 : 0]
-                                          [regen ? 1 : 0];
-        if (cached == 0) cached = shade_blocks_per_cu(ctx->S, regen);
+                                          [mode];
+        if (cached == 0) cached = shade_blocks_per_cu(ctx->S, mode);
         const int bpc = shade_bpc_env ? (int)shade_bpc_env : cached;
         return (ctx->num_cu * bpc + seg_blocks - 1) / seg_blocks * seg_blocks;
     };
@@ -967,7 +976,9 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, kCtrlWords * sizeof(uint32_t), s));
         const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
         const bool regen = n_seed < chunk_items;  // else the seed claimed every item of the chunk
-        const int grid_shade = grid_shade_of(regen);
+        // the lean 24-B path state: L stays 0 until the path ends, item = slot
+        ctx->wb.lean = (!regen && ctx->lean_scene && !ctx->no_lean) ? 1u : 0u;
+        const int grid_shade = grid_shade_of(shade_mode(regen, ctx->wb.lean != 0u));
         HIP_TRY(ctx, launch_wf_seed(ctx->C, Rc, B, n_seed, chunk_items, ctx->d_stats, s));
         for (uint32_t it = 0;; ++it) {
             if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
@@ -1358,6 +1369,8 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     if (drain_env && *drain_env) ctx->drain_rays = (uint32_t)std::strtoul(drain_env, nullptr, 10);
     const char *beam_env = std::getenv("OCTPT_BEAM");
     ctx->beam = !(beam_env && beam_env[0] == '0');
+    const char *lean_env = std::getenv("OCTPT_LEAN");
+    ctx->no_lean = lean_env && lean_env[0] == '0';
     ctx->drain_models = env_u32("OCTPT_DRAIN_MODELS", 0u) != 0u;
     ctx->mem_limit = (size_t)env_u32("OCTPT_DEVICE_MEM_LIMIT", 0u) << 20;  // MiB, test hook (ensure_wave)
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
@@ -1899,6 +1912,7 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
             tot.chunk_items = std::max(tot.chunk_items, cs.chunk_items);
             tot.wave_allocs += cs.wave_allocs;
             tot.beam_restarts += cs.beam_restarts;
+            tot.hit_check_failures += cs.hit_check_failures;
         }
         tot.build_ms = std::max(tot.build_ms, (double)ctx->build_ms);  // the builder runs on the first device
         tot.launches = ctx->launches;
@@ -1966,6 +1980,8 @@ octpt_status octpt_get_stats(const octpt_ctx *cctx, octpt_stats *out) {
     out->block_tests = v[kStatBlockTests];
     out->issued_bytes = v[kStatIssued];
     out->beam_restarts = redo_main + redo_drain;
+    out->hit_check_failures = 0;
+    for (uint32_t r = 0; r < 2u * kSegs; ++r) out->hit_check_failures += rows[r * kStatRow + kStatHitCheckWord];
     out->pool_slots = ctx->pool;
     out->chunk_items = ctx->color_cap;
     out->wave_allocs = ctx->wave_allocs_n;

@@ -188,7 +188,12 @@ struct WaveBuffers {
     // (camera eye.xyz, kPrimNone): the first half of every ray record the seed writes, which the
     // chunk's first shade takes from here instead of re-reading it
     float4 eye;
+    // the lean 24-B path state (pa = (T, rng), pc; pb and item0 unused): no emitters, no sun sampling and the
+    // pool holding the chunk (item = slot), set per chunk by the host
+    uint32_t lean;
 };
+// shade instance: 0 = 40-B path state, 1 = with regeneration (pool smaller than the chunk), 2 = lean
+inline int shade_mode(bool regen, bool lean) { return regen ? 1 : (lean ? 2 : 0); }
 
 // per-launch statistics, accumulated with one atomic per wave
 enum StatIndex {
@@ -212,6 +217,8 @@ constexpr uint32_t kStatDrainRow = kSegs;
 // beam-started rays traced again from the cube entry (octpt_stats::beam_restarts): a word of the row
 // past the kStatCount counters, counted by one atomic per event
 constexpr uint32_t kStatBeamRestartWord = 10;
+// hit records with an unwritten field (OCTPT_CHECK_HITS diagnostic builds; octpt_stats::hit_check_failures)
+constexpr uint32_t kStatHitCheckWord = 11;
 static_assert(kStatBeamRestartWord >= kStatCount && kStatBeamRestartWord < 12, "below the lane-profile words");
 
 // Multi-device renders (octpt_create_multi): item i of a shard's compact tile order (tile
@@ -251,8 +258,8 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
                            uint32_t chunk_items, bool first, bool regen, int grid, unsigned long long *stats,
                            hipStream_t stream);
-// blocks per CU of the shade instance (registers bound it; shade uses no dynamic LDS)
-int shade_blocks_per_cu(const DevScene &S, bool regen);
+// blocks per CU of the shade instance (shade_mode; registers bound it, shade uses no dynamic LDS)
+int shade_blocks_per_cu(const DevScene &S, int mode);
 // whether the scene's shade instance copies the material / texture tables into LDS
 bool shade_lds_tables(const DevScene &S);
 // the drain of a chunk's last queued rays (every chunk item claimed): one launch, paths finished in-lane

@@ -323,6 +323,32 @@ __device__ __forceinline__ uint2 hit_record(uint32_t prim, const PrimHit &h) {
     return make_uint2((prim & kPrimCuboidBit) | ((h.f & 15u) << 27) | (prim & kPrimIndexMask), __float_as_uint(h.t));
 }
 
+// OCTPT_CHECK_HITS (the diagnostic build liboctpt_checkhits.so): every step's PrimHit starts with
+// sentinel fields, and a hit whose record fields (the ones shade reads) still hold the sentinel is counted
+// (octpt_stats.hit_check_failures): a field the path that produced the hit did not write, or a codegen merge
+// that let the lane keep the value it entered the step with (the block-leaf defect of round 3).
+#ifdef OCTPT_CHECK_HITS
+constexpr uint32_t kHitSentinel = 0x7FC0DEADu;  // a NaN payload no hit computation produces
+#define HIT_POISON(h) ((h).t = (h).u = (h).v = __uint_as_float(kHitSentinel), (h).f = kHitSentinel)
+template <int kPrims>
+__device__ __forceinline__ bool hit_unwritten(uint32_t prim, const PrimHit &h) {
+    if (prim == kPrimNone) return true;
+    if (kPrims == kPrimsBlocks)  // (face << 27 | block or the quad, t) + (u, v)
+        return __float_as_uint(h.t) == kHitSentinel || __float_as_uint(h.u) == kHitSentinel ||
+               __float_as_uint(h.v) == kHitSentinel;
+    if (!(prim & kPrimCuboidBit)) return h.f == kHitSentinel;  // a sphere: its root flag (t is recomputed)
+    return h.f == kHitSentinel || __float_as_uint(h.t) == kHitSentinel;  // a cuboid: face flags and t
+}
+#define HIT_CHECK(kP, rs, prim, h, stats, row_base)                                                                  \
+    do {                                                                                                        \
+        if ((rs) == kStepHit && hit_unwritten<kP>((prim), (h)))                                                  \
+            atomicAdd(&(stats)[((row_base) + blockIdx.x % kSegs) * kStatRow + kStatHitCheckWord], 1ull);           \
+    } while (0)
+#else
+#define HIT_POISON(h) ((void)0)
+#define HIT_CHECK(kP, rs, prim, h, stats, row_base) ((void)0)
+#endif
+
 // Sphere::hit restated (sphere.rs:33-57) + root selection [C2].  The square root and divisions
 // run only for lanes that can still hit: 48 % of C3's sphere tests have disc < 0 and 28 % are
 // self tests, mostly of rays leaving outward, so the wave usually skips that block.
@@ -537,11 +563,13 @@ __device__ inline bool block_leaf_test(const DevScene &S, const TraceRay &r, con
         ISSUED(cnt, 4);
         uint32_t q = 0u;
         float al = 0.0f, be = 0.0f;
-        if (!model_test(S, r, voxel, mdl, t_accept, h.t, q, al, be, cnt)) return false;
+        const bool found = model_test(S, r, voxel, mdl, t_accept, h.t, q, al, be, cnt);
+        // the hit fields are written on both paths, not after a divergent return (fields
+        // written only after the alpha test's divergent branch were left stale on passing lanes, round 3)
         prim = kPrimCuboidBit | q;
         h.u = al;
         h.v = be;
-        return true;
+        return found;
     }
     if (E.t_min == 0.0f) return false;
     const float inv_se = __uint_as_float(0x7F000000u - __float_as_uint(se));  // 1 / scale_exp2, exact
@@ -1798,10 +1826,20 @@ __device__ __forceinline__ void pack_path(const PathState &ps, uint32_t item, fl
     c = make_uint2(ps.cur, ps.depth | (ps.specular ? 1u << 8 : 0u) | (ps.shadow ? 1u << 9 : 0u) | (ps.branch << 10) |
                                (ps.path_segs << 16) | (ps.seg_base << 23));
 }
+// kLean (WaveBuffers::lean): the 24-B path state (T, rng) + (cur, bits).  The radiance L of a
+// path that continues is exactly 0 when the scene has no emitters and no sun sampling (it is added only at the
+// path's end, sky on a miss), and its item equals its slot when the pool holds the chunk (the direct seeding):
+// neither is stored, 16 B less written and read per segment.
+template <bool kLean = false>
 __device__ __forceinline__ void store_path(const WaveBuffers &B, uint32_t slot, const PathState &ps, uint32_t item) {
     float4 a, b;
     uint2 c;
     pack_path(ps, item, a, b, c);
+    if (kLean) {
+        B.pa[slot] = make_float4(a.x, a.y, a.z, b.z);  // (T, rng)
+        B.pc[slot] = c;
+        return;
+    }
     B.pa[slot] = a;
     B.pb[slot] = b;
     B.pc[slot] = c;
@@ -1846,8 +1884,15 @@ __device__ __forceinline__ void unpack_path(float4 a, float4 b, uint2 c, float4 
     ps.path_segs = (c.y >> 16) & 127u;
     ps.seg_base = c.y >> 23;
 }
+template <bool kLean = false>
 __device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, float4 r0, float4 r1, PathState &ps,
                                           uint32_t &item) {
+    if (kLean) {  // L = +0 as the path started, item = slot (store_path<true>)
+        const float4 a = B.pa[slot];
+        unpack_path(make_float4(a.x, a.y, a.z, 0.0f), make_float4(0.0f, 0.0f, a.w, __uint_as_float(slot)), B.pc[slot],
+                    r0, r1, ps, item);
+        return;
+    }
     unpack_path(B.pa[slot], B.pb[slot], B.pc[slot], r0, r1, ps, item);
 }
 
@@ -1885,8 +1930,11 @@ __device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const W
         item_pixel(R, item % R.total_items, x, y);
         ps.beam = R.beam[(y / kBeamTile) * R.beam_tx + x / kBeamTile];
     }
-    if (kSeed) B.item0[slot] = item;
-    else store_path(B, slot, ps, item);
+    if (kSeed) {
+        if (!B.lean) B.item0[slot] = item;  // lean: the chunk's first shade takes item = slot
+    } else {
+        store_path(B, slot, ps, item);
+    }
     return true;
 }
 
@@ -2104,8 +2152,10 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
             if (active) {
                 uint32_t prim = kPrimNone;
                 PrimHit h;
+                HIT_POISON(h);
                 const int rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
                 if (rs != kStepContinue) {
+                    HIT_CHECK(kPrims, rs, prim, h, stats, 0u);
                     // the record's address is formed here from pos (through an empty asm), not kept
                     // from the refill in two more registers that the loop would spill (not in the
                     // sphere instance, whose allocation is better off as it is: C3 -1 % with it)
@@ -2137,14 +2187,14 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
 // it finished (its colour record written).  first (wave-uniform: the chunk's first shade, whose
 // rays the seed started): the path state is rebuilt from the slot's item as the seed computed it,
 // through the same pack / unpack as a stored path, instead of being read.
-template <bool kNee>
+template <bool kNee, bool kLean = false>
 __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C, const DevRender &R,
                                            const WaveBuffers &B, bool first, float4 r0, float4 r1, const uint2 *hit_rec,
                                            const float2 *huv_rec, PathState &ps, uint32_t &slot, uint32_t &item,
                                            Counters &cnt) {
     slot = __float_as_uint(r1.w) & (kRayBeamBit - 1u);
     if (first) {
-        item = B.item0[slot];
+        item = kLean ? slot : B.item0[slot];
         PathState s0;
         item_path(C, R, item, s0);  // the seed only queued items inside the image
         float4 a, b;
@@ -2152,14 +2202,14 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
         pack_path(s0, item, a, b, c);
         unpack_path(a, b, c, B.eye, r1, ps, item);  // a camera ray's ray0 is (eye, kPrimNone): not re-read
     } else {
-        load_path(B, slot, r0, r1, ps, item);
+        load_path<kLean>(B, slot, r0, r1, ps, item);
     }
     const uint2 hr = *hit_rec;
     if (__builtin_expect((hr.x == kPrimNone) & (hr.y == kHitRetrace), 0)) {
         // a beam-started camera ray that reached the reference's step cap (extend, esvo_beam_capped): the
         // same ray is queued again without its beam start, for the walk from the cube entry.  No segment
         // is counted; the path state is the seed's (stored now when this shade rebuilt it from the item).
-        if (first) store_path(B, slot, ps, item);
+        if (first) store_path<kLean>(B, slot, ps, item);
         ps.n = V(0.0f, 0.0f, 0.0f);
         ps.beam = 0.0f;
         cnt.redo++;
@@ -2185,7 +2235,7 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     bool cont = shade_segment<kNee>(S, R, ps, hit, cnt);
     if (cont) cont = begin_segment(ps);
     if (cont) {
-        store_path(B, slot, ps, item);
+        store_path<kLean>(B, slot, ps, item);
         if (kNee && ps.shadow) {  // a shadow segment follows: new sun sample or the next one
             if (!was_shadow) store_nee(B, slot, ps);
             store_att(B, slot, ps);
@@ -2203,6 +2253,9 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
 #ifndef OCTPT_SHADE_WAVES
 #define OCTPT_SHADE_WAVES 1
 #endif
+#ifndef OCTPT_SHADE_LEAN_WAVES
+#define OCTPT_SHADE_LEAN_WAVES 6  // the lean instance (kMode 2): register budget for 6 waves/SIMD (A/B knob)
+#endif
 // scenes with at most kShadeLdsMats materials and textures shade from LDS copies of the material
 // and texture tables and the sRGB LUT: these loads sit at the end of the dependent chain
 // ray -> path state / primitive -> face material -> material -> texture -> texel -> LUT
@@ -2218,8 +2271,10 @@ constexpr uint32_t kShadeLdsBlocks = OCTPT_SHADE_LDS_BLOCKS;
 // kRegen: finished lanes regenerate their slot with the next chunk items.  Only a pool smaller than
 // the chunk needs it (when the pool holds the chunk -- C3's frame, every 4K chunk -- the seed claimed
 // every item); the instance without it is 19 VGPRs leaner (96 instead of 115, 5 waves/SIMD instead of 4).
-template <bool kNee, bool kLdsMats, bool kRegen>
-__global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
+// kMode: 0 = the 40-B path state, no regeneration; 1 = with regeneration; 2 = the lean 24-B path state (no
+// regeneration, no sun sampling, kLean above)
+template <bool kNee, bool kLdsMats, int kMode>
+__global__ __launch_bounds__(kBlock, kMode == 2 ? OCTPT_SHADE_LEAN_WAVES : OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items, uint32_t first,
                                                           unsigned long long *__restrict__ stats) {
     constexpr uint32_t kT = (kLdsMats && kShadeLdsMats) ? kShadeLdsMats : 1u;
@@ -2263,11 +2318,12 @@ __global__ __launch_bounds__(kBlock, OCTPT_SHADE_WAVES) void wf_shade_kernel(Dev
         if (valid) {
             const float4 r1 = B.ray1[q][i];
             const float4 r0 = first ? B.eye : B.ray0[q][i];  // (the chunk's first shade: the seed's camera rays)
-            append = shade_lane<kNee>(S, C, R, B, first != 0u, r0, r1, B.hit + i, B.huv + i, ps, slot, item, cnt);
+            append = shade_lane<kNee, kMode == 2>(S, C, R, B, first != 0u, r0, r1, B.hit + i, B.huv + i, ps, slot, item,
+                                                  cnt);
             finished = !append;
         }
         // regenerate: finished lanes take the next chunk items (path regeneration)
-        if constexpr (kRegen) {
+        if constexpr (kMode == 1) {
             if (regen(C, R, B, slot, finished, chunk_items, cur, ps, cnt)) append = true;
         }
         const uint32_t t = wave_ticket(B.ctrl + ctr_count(q ^ 1u, seg), append);
@@ -2308,8 +2364,10 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                 int rs;
                 for (;;) {
                     do {
+                        HIT_POISON(h);
                         rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
                     } while (rs == kStepContinue);
+                    HIT_CHECK(kPrims, rs, prim, h, stats, kStatDrainRow);
                     cnt.steps += esvo_executed(E.iter);
                     if (!((rs == kStepMiss) & esvo_beam_capped(E.iter))) break;
                     cnt.redo++;  // traced again from the cube entry, in place (shade_lane's retrace, inline)
@@ -2325,7 +2383,10 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                 const float2 huv = make_float2(h.u, h.v);
                 PathState ps;
                 uint32_t slot, item;
-                if (!shade_lane<kNee>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item, cnt)) break;
+                const bool cont = (!kNee && B.lean)
+                                      ? shade_lane<kNee, true>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item, cnt)
+                                      : shade_lane<kNee, false>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item, cnt);
+                if (!cont) break;
                 // the next segment's ray record, as store_ray writes it
                 r0 = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.last_prim));
                 r1 = make_float4(ps.d.x, ps.d.y, ps.d.z,
@@ -2677,22 +2738,23 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
     return hipGetLastError();
 }
 
-// the shade instance a scene and chunk launch (sun sampling, LDS material tables, regeneration)
+// the shade instance a scene and chunk launch (sun sampling, LDS material tables, regeneration, lean state)
 template <bool kNee, bool kLds>
-static const void *shade_instance_of(bool regen) {
-    return regen ? reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, true>)
-                 : reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, false>);
+static const void *shade_instance_of(int mode) {
+    if (!kNee && mode == 2) return reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2>);
+    return mode == 1 ? reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, 1>)
+                     : reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, 0>);
 }
 bool shade_lds_tables(const DevScene &S) { return S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats; }
-static const void *shade_instance(const DevScene &S, bool regen) {
+static const void *shade_instance(const DevScene &S, int mode) {
     const bool lds = shade_lds_tables(S);
-    return S.sun.sun_sampling ? (lds ? shade_instance_of<true, true>(regen) : shade_instance_of<true, false>(regen))
-                              : (lds ? shade_instance_of<false, true>(regen) : shade_instance_of<false, false>(regen));
+    return S.sun.sun_sampling ? (lds ? shade_instance_of<true, true>(mode) : shade_instance_of<true, false>(mode))
+                              : (lds ? shade_instance_of<false, true>(mode) : shade_instance_of<false, false>(mode));
 }
 
-int shade_blocks_per_cu(const DevScene &S, bool regen) {
+int shade_blocks_per_cu(const DevScene &S, int mode) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, shade_instance(S, regen), kBlock, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, shade_instance(S, mode), kBlock, 0) != hipSuccess)
         return 4;
     return blocks > 0 ? blocks : 1;
 }
@@ -2703,7 +2765,8 @@ hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRende
     uint32_t first_u = first ? 1u : 0u;
     void *args[] = {const_cast<DevScene *>(&S), const_cast<DevCamera *>(&C), const_cast<DevRender *>(&R),
                     const_cast<WaveBuffers *>(&B), &q, &chunk_items, &first_u, &stats};
-    const hipError_t e = hipLaunchKernel(shade_instance(S, regen), dim3(grid), dim3(kBlock), args, 0, stream);
+    const hipError_t e = hipLaunchKernel(shade_instance(S, shade_mode(regen, B.lean != 0u)), dim3(grid), dim3(kBlock),
+                                         args, 0, stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -806,8 +806,11 @@ def step_cap_world(scene: Scene, seed: int, floor_len: int = 1024, floor_w: int 
     """A block-value world whose near-horizontal camera rays reach the reference's ESVO step
     cap (OCTREE_MAX_STEPS = 1000, octree_traversal.rs:13, 127) and miss: a checkerboard floor of blocks at
     y = 0 (every level-1 octant along the floor is present, so a ray skimming over it at 1 < y < 2 spends
-    ~2 iterations per unit of distance without meeting a leaf) and a stone wall at x = wall_x that only a
-    walk counting fewer iterations than the reference would reach.  Sets scene.blocks / cells."""
+    ~2 iterations per unit of distance without meeting a leaf), a stone wall at x = wall_x that only a
+    walk counting fewer iterations than the reference would reach, and a picket of stone posts at x = 0,
+    y = 1 (every fourth z): a camera tile whose pyramid grazes a post starts its rays right there, with a
+    small bound of skipped iterations, and those of its rays that pass the post run into the cap after the
+    start (the restart of a beam-started ray).  Sets scene.blocks / cells."""
     mat = block_materials(scene, seed)
     scene.blocks = np.array([[mat["grass_side"]] * 2 + [mat["dirt"], mat["grass_top"]] + [mat["grass_side"]] * 2,
                              [mat["stone"]] * 6], np.uint32)
@@ -817,7 +820,9 @@ def step_cap_world(scene: Scene, seed: int, floor_len: int = 1024, floor_w: int 
     floor = np.stack([xx[keep], np.zeros(keep.sum(), np.int64), zz[keep], np.zeros(keep.sum(), np.int64)], 1)
     wx, wy, wz = np.meshgrid(np.arange(wall_x, wall_x + 4), np.arange(8), np.arange(floor_w), indexing="ij")
     wall = np.stack([wx.ravel(), wy.ravel(), wz.ravel(), np.ones(wx.size, np.int64)], 1)
-    scene.cells = np.concatenate([floor, wall]).astype(np.uint32)
+    pz = np.arange(0, floor_w, 4)
+    posts = np.stack([np.zeros_like(pz), np.ones_like(pz), pz, np.ones_like(pz)], 1)
+    scene.cells = np.concatenate([floor, wall, posts]).astype(np.uint32)
     return scene
 
 

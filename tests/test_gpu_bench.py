@@ -33,3 +33,17 @@ def test_two_ranks_gather_equals_one(tmp_path):
     assert np.array_equal(f1, f2)
     # every rank's segments are counted once
     assert one["config"]["segments_per_step"] == two["config"]["segments_per_step"]
+    # rank 0's measurement of the same frame through one multi-device context (octpt_create_multi):
+    # on this box its two entries repeat device 0
+    cm = two["capi_multi"]
+    assert "error" not in cm, cm
+    assert cm["devices"] == [0, 0] and cm["segments"] == one["config"]["segments_per_step"] and cm["value"] > 0
+
+
+def test_capi_devices_bench(tmp_path):
+    """bench.py --capi-devices 2: the whole frame through one two-entry context equals the one-context frame."""
+    one, f1 = _bench(tmp_path, 1)
+    two, f2 = _bench(tmp_path, 1, ("--capi-devices", "2"))
+    assert two["config"]["parallelism"] == "capi-multi2" and two["config"]["capi_devices"] == [0, 0]
+    assert np.array_equal(f1, f2)
+    assert one["config"]["segments_per_step"] == two["config"]["segments_per_step"]
