@@ -1394,6 +1394,15 @@ octpt_status octpt_create_multi(const int32_t *devices, uint32_t n, octpt_ctx **
     *out = nullptr;
     if (!devices || n == 0 || n > 64) return OCTPT_ERR_INVALID_ARG;
     if (n == 1) return octpt_create(devices[0], out);
+    int caller_device = 0;
+    const bool restore = hipGetDevice(&caller_device) == hipSuccess;
+    struct Restore {  // the calling thread's current device is left as it was
+        bool on;
+        int dev;
+        ~Restore() {
+            if (on) (void)hipSetDevice(dev);
+        }
+    } restore_device{restore, caller_device};
     try {
         octpt_ctx *ctx = nullptr;
         octpt_status st = octpt_create(devices[0], &ctx);  // the first entry's device holds the caller's buffers

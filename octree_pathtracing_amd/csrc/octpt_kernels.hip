@@ -230,20 +230,18 @@ struct Esvo {
     uint32_t parent, pmask, idx, mirror, iter;  // scale = exponent of scale_exp2 + OCTREE_MAX_SCALE - 127
 };
 
-// E.iter: the low 16 bits are the iteration count the reference's cap applies to (OCTREE_MAX_STEPS,
-// octree_traversal.rs:127); the high 16 bits are the iteration bound a beam start begins the count at
-// (esvo_begin, beam_kernel), 0 for every other ray.  Executed iterations = low - high.
-__device__ __forceinline__ bool esvo_capped(uint32_t it) { return (uint16_t)it >= (uint16_t)OCTREE_MAX_STEPS; }
-__device__ __forceinline__ uint32_t esvo_executed(uint32_t it) { return (it & 0xFFFFu) - (it >> 16); }
-// a beam-started ray that reached the cap: the reference may still have had iterations left (the bound
-// over-counts the ones the beam skipped), so the ray is traced again from its cube entry
-__device__ __forceinline__ bool esvo_beam_capped(uint32_t it) { return (it >> 16) != 0u && esvo_capped(it); }
+// E.iter: the iteration count the reference's cap applies to (OCTREE_MAX_STEPS, octree_traversal.rs:127).
+// A beam-started ray's count begins at beam_kernel's bound of the iterations its start skipped (esvo_begin):
+// its caller subtracts that bound from the executed-iteration statistic when the ray begins.  A beam-started
+// ray that reaches the cap may still have had iterations left in the reference (the bound over-counts the
+// skipped ones), so it is traced again from its cube entry (extend's kHitCapped record, shade's retrace).
+__device__ __forceinline__ bool esvo_capped(uint32_t it) { return it >= OCTREE_MAX_STEPS; }
 
 struct Counters {
     uint32_t paths, segs, steps, sph, cub, shade, tex;
     uint32_t blk;  // block-value leaf tests (C23)
     uint32_t ib;   // issued load bytes of extend (OCTPT_COUNT_ISSUED builds; see ISSUED below)
-    uint32_t redo;  // beam-started rays traced again from the cube entry (esvo_beam_capped; stat word kStatBeamRestartWord)
+    uint32_t redo;  // beam-started rays traced again from the cube entry (the step cap; stat word kStatBeamRestartWord)
 #ifdef OCTPT_PROFILE_LANES  // diagnostic builds: per-wave lane occupancy of extend's step (stat words 8..)
     uint32_t p_iters, p_active, p_leaf_it, p_leaf_ln, p_pop_it, p_pop_ln, p_push_it, p_desc_ln, p_exact, p_fold_it,
         p_fold_ln, p_dfold_it, p_dfold_ln;
@@ -809,7 +807,7 @@ __device__ __forceinline__ void esvo_first_child(Esvo &E) {
 
 // ESVO's state at the cube entry from the ray's t_coef / t_bias / mirror (octree_traversal.rs:79-112; the
 // first child follows, esvo_first_child): the walk of the reference from its first iteration.  Also how a
-// beam-started ray that reached the step cap starts again (esvo_beam_capped): its t_coef, t_bias and
+// beam-started ray that reached the step cap starts again (the drain's restart): its t_coef, t_bias and
 // mirror are the ray's own, only the walk restarts.
 __device__ __forceinline__ void esvo_root(const DevScene &S, Esvo &E) {
     E.parent = S.root;
@@ -829,7 +827,7 @@ __device__ __forceinline__ void esvo_root(const DevScene &S, Esvo &E) {
 // rays near-parallel to an axis), clamped to the cube exit.  The low kBeamIterBits of t_start's bits
 // hold a bound of the reference iterations before the start (beam_kernel), at which the iteration
 // count begins, so that the reference's step cap still applies (a ray reaching it is traced again from
-// its cube entry, esvo_beam_capped).
+// its cube entry, esvo_capped).
 template <uint32_t kS>
 __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk,
                                   float t_start = 0.0f) {
@@ -865,8 +863,7 @@ __device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &
         E.t_min = tmx(E.t_min, tmn(t_start - margin, E.t_max));
         // the reference's step cap counts from the cube entry: the count starts at beam_kernel's bound
         // of the iterations skipped (carried in t_start's low mantissa bits, beam_pack)
-        const uint32_t skipped = __float_as_uint(t_start) & kBeamIterMask;
-        E.iter = skipped | (skipped << 16);
+        E.iter = __float_as_uint(t_start) & kBeamIterMask;
     }
     esvo_first_child(E);
 }
@@ -1801,9 +1798,10 @@ __global__ __launch_bounds__(kBlock, OCTPT_PREVIEW_WAVES_OF(kPrims)) void previe
 //   pa[slot]   = (T.xyz, L.x)  pb[slot] = (L.y, L.z, rng, item)  pc[slot] = (cur_mat, depth | spec<<8 | segs<<16)
 //   a camera ray with a beam start: ray1 bit 30 set, ray0.w = the start t (its last_prim is kPrimNone)
 constexpr uint32_t kRayBeamBit = 0x40000000u;  // slots < 2^30 (the pool cap)
-// a miss record's second word for a beam-started ray that reached the reference's step cap: shade queues
-// the same ray again without its beam start (the walk from the cube entry), no segment counted
-constexpr uint32_t kHitRetrace = 1u;
+// a miss record's second word for a ray that ended on the reference's step cap: for a beam-started camera
+// ray (its record's kRayBeamBit) shade queues the same ray again without its start (the walk from the cube
+// entry), no segment counted; any other such ray is the reference's miss
+constexpr uint32_t kHitCapped = 1u;
 __device__ __forceinline__ void store_ray(const WaveBuffers &B, uint32_t q, uint32_t pos, uint32_t slot,
                                           const PathState &ps) {
     const bool beam = ps.beam > 0.0f && ps.path_segs == 1u;
@@ -2127,6 +2125,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                     tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), ray_last_prim(r0, r1),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk, ray_beam(r0, r1));
+                    cnt.steps -= E.iter;  // a beam start's bound of skipped iterations: executed ones are counted
                     active = true;
                 }
             }
@@ -2138,7 +2137,8 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 // than kShortRaySteps ESVO steps, the wave refills 32 at a time, else 16
                 // (a lane's rays counted as the wave's average, segs_w / 64: no per-lane counter, which
                 // the block instance spilled to scratch at every refill)
-                const bool short_rays = cnt.steps * 64u < kShortRaySteps * segs_w;
+                // (signed: a lane's in-flight beam start has been subtracted already)
+                const bool short_rays = (int32_t)cnt.steps * 64 < (int32_t)(kShortRaySteps * segs_w);
                 thr = __popcll(__ballot(short_rays)) > 32 ? OCTPT_THR_SHORT : OCTPT_THR_LONG;
             }
         }
@@ -2161,16 +2161,16 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                     // sphere instance, whose allocation is better off as it is: C3 -1 % with it)
                     uint32_t p = pos;
                     if constexpr (kPrims != kPrimsSpheres) asm volatile("" : "+v"(p));
-                    // a miss: (kPrimNone, 0), or (kPrimNone, kHitRetrace) for a beam-started ray that reached
-                    // the step cap, which shade queues again without its beam start (esvo_beam_capped)
-                    const uint2 miss = make_uint2(kPrimNone, esvo_beam_capped(E.iter) ? kHitRetrace : 0u);
+                    // a miss: (kPrimNone, 0), or (kPrimNone, kHitCapped) on the step cap (shade retraces a
+                    // beam-started camera ray, esvo_capped)
+                    const uint2 miss = make_uint2(kPrimNone, esvo_capped(E.iter) ? kHitCapped : 0u);
                     if constexpr (kPrims == kPrimsBlocks) {  // (face << 27 | block or the quad, t) + (u, v) (C23)
                         B.hit[p] = rs == kStepHit ? make_uint2(prim, __float_as_uint(h.t)) : miss;
                         if (rs == kStepHit) B.huv[p] = make_float2(h.u, h.v);
                     } else {
                         B.hit[p] = rs == kStepHit ? hit_record(prim, h) : miss;
                     }
-                    cnt.steps += esvo_executed(E.iter);
+                    cnt.steps += E.iter;
                     active = false;
                 }
             }
@@ -2205,8 +2205,8 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
         load_path<kLean>(B, slot, r0, r1, ps, item);
     }
     const uint2 hr = *hit_rec;
-    if (__builtin_expect((hr.x == kPrimNone) & (hr.y == kHitRetrace), 0)) {
-        // a beam-started camera ray that reached the reference's step cap (extend, esvo_beam_capped): the
+    if (__builtin_expect((hr.x == kPrimNone) & (hr.y == kHitCapped) & ((__float_as_uint(r1.w) & kRayBeamBit) != 0u), 0)) {
+        // a beam-started camera ray that reached the reference's step cap (extend's kHitCapped record): the
         // same ray is queued again without its beam start, for the walk from the cube entry.  No segment
         // is counted; the path state is the seed's (stored now when this shade rebuilt it from the item).
         if (first) store_path<kLean>(B, slot, ps, item);
@@ -2359,6 +2359,8 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                                                    (__float_as_uint(r1.w) >> 31) != 0u);
                 Esvo E;
                 esvo_begin(S, tr, E, stk, ray_beam(r0, r1));
+                cnt.steps -= E.iter;  // as in wf_extend_kernel
+                bool beam_ray = (__float_as_uint(r1.w) & kRayBeamBit) != 0u;
                 uint32_t prim = kPrimNone;
                 PrimHit h;
                 int rs;
@@ -2368,9 +2370,10 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                         rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
                     } while (rs == kStepContinue);
                     HIT_CHECK(kPrims, rs, prim, h, stats, kStatDrainRow);
-                    cnt.steps += esvo_executed(E.iter);
-                    if (!((rs == kStepMiss) & esvo_beam_capped(E.iter))) break;
+                    cnt.steps += E.iter;
+                    if (!((rs == kStepMiss) & esvo_capped(E.iter) & beam_ray)) break;
                     cnt.redo++;  // traced again from the cube entry, in place (shade_lane's retrace, inline)
+                    beam_ray = false;
                     esvo_root(S, E);
                     esvo_first_child(E);
                 }

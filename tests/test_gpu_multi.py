@@ -128,3 +128,40 @@ def test_multi_beam_on(torch_cuda):
     _same(gpu_render(torch_cuda, two, sc, cam, rs), gpu_render(torch_cuda, one, sc, cam, rs), "beam x2")
     two.close()
     one.close()
+
+
+def test_multi_poll_cancel_and_errors(torch_cuda, multi3):
+    """FrameInFlight on a three-entry context: poll until ready, cancel a long frame (every entry's render
+    stops, the accumulation is untouched), and an entry's error reaches the caller with its message."""
+    from octree_pathtracing_amd import _lib
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import FrameInFlightPoll
+
+    sc, cam, rs = S.make_config("tiny")
+    multi3.set_scene(sc)
+    multi3.set_camera(cam)
+    multi3.set_resolution((rs.width, rs.height))
+    multi3.max_depth, multi3.seed = rs.max_depth, rs.seed
+    multi3.reset_render()
+    f = multi3.render_frame(spp_count=rs.spp)
+    while True:
+        state, payload = f.poll()
+        if state is not FrameInFlightPoll.NotReady:
+            break
+    assert state is FrameInFlightPoll.Ready and multi3.get_current_spp() == rs.spp
+    before = multi3.get_float_image().copy()
+    f2 = multi3.render_frame(spp_count=512)
+    f2.cancel()
+    while True:
+        state, payload = f2.poll()
+        if state is not FrameInFlightPoll.NotReady:
+            break
+    assert state is FrameInFlightPoll.Cancelled and payload is None
+    assert multi3.get_current_spp() == rs.spp
+    assert np.array_equal(multi3.get_float_image().view(np.uint32), before.view(np.uint32))
+    # a branch schedule that does not end on a pass boundary is refused by every entry (C20)
+    multi3.branch_count = 10
+    rs.spp = 5  # passes of weight 1, 1, 1, 1, then 6: 5 samples end inside a pass
+    with pytest.raises(_lib.OctptError, match="pass boundary"):
+        multi3.render(rs)
+    multi3.branch_count = 1
