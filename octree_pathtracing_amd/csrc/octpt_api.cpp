@@ -116,16 +116,8 @@ struct octpt_ctx {
     std::vector<std::pair<void *, size_t>> wave_sizes;
     uint64_t wave_allocs_n = 0;  // successful (re)allocations of the queues + path state
     bool oom_warned = false;
-    uint32_t *h_count = nullptr;  // pinned rings (one per wavefront lane): the segment counters after each iteration's shade
-    hipEvent_t count_ev[2][kLookahead + 1] = {};
-    // wavefront lanes (OCTPT_LANES=2): the chunk's items split into two halves, each a
-    // complete wavefront (its own 64 queue segments and counters) stepping on its own stream (the
-    // caller's and lane_stream), so one half's extend tail and launch gaps overlap the other half's
-    // work.  fork_ev orders lane 1 after the seed, join_ev the resolve after lane 1.
-    uint32_t lanes = 1;
-    bool lane_full_grid = false;  // OCTPT_LANE_GRID=full: each lane's extend launch takes the whole grid (A/B)
-    hipStream_t lane_stream = nullptr;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
+    hipEvent_t count_ev[kLookahead + 1] = {};
     uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
     bool beam = true;  // camera rays start at their tile's beam (OCTPT_BEAM=0: off)
     uint32_t drain_rays = kDefaultDrainRays;  // queue length at which the drain takes over (OCTPT_DRAIN_RAYS, 0 = off)
@@ -659,7 +651,6 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     R.subs = nullptr;
     R.beam = nullptr;
     R.beam_tx = (p->width + kBeamTile - 1) / kBeamTile;
-    R.item_base = R.slot_base = 0u;  // set per wavefront lane (enqueue_wavefront)
     if (B > 1u && !(p->flags & OCTPT_RENDER_PREVIEW)) {
         // TileRenderer pass schedule (tile_renderer.rs:416-484, C20): the call covers whole passes
         if (p->flags & OCTPT_RENDER_MEGAKERNEL)
@@ -766,10 +757,9 @@ enum OomPart { kOomNone = 0, kOomQueues, kOomColor, kOomNee };
 octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool nee, bool blocks, OomPart *part) {
     *part = kOomNone;
     if (!ctx->h_count) {
-        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), 2 * (kLookahead + 1) * kCountSpan * sizeof(uint32_t),
+        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), (kLookahead + 1) * kCountSpan * sizeof(uint32_t),
                                    hipHostMallocDefault));
-        for (auto &lane : ctx->count_ev)
-            for (auto &ev : lane) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        for (auto &ev : ctx->count_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
     if (pool > ctx->pool) {
         HIP_TRY(ctx, hipDeviceSynchronize());
@@ -778,9 +768,7 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
         // queues + path state: 116 B per slot
         size_t want = pool;
         for (;;) {
-            // (two lanes: each lane's half of every queue holds half the pool; the whole
-            // queue, seg_cap per segment, still holds the pool for a chunk run as one lane)
-            B.seg_cap = (uint32_t)(ctx->lanes == 2 ? 2 * seg_cap_for((want + 1) / 2) : seg_cap_for(want));
+            B.seg_cap = (uint32_t)seg_cap_for(want);
             const size_t qlen = (size_t)kSegs * B.seg_cap;  // queue positions
             hipError_t e = wave_alloc(ctx, qlen, &B.ray0[0]);
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.ray0[1]);
@@ -791,7 +779,7 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
             if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pc);
             if (e == hipSuccess) e = wave_alloc(ctx, want, &B.item0);
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.hit);
-            if (e == hipSuccess) e = wave_alloc(ctx, 2 * kCtrlWords, &B.ctrl);  // one counter block per lane
+            if (e == hipSuccess) e = wave_alloc(ctx, kCtrlWords, &B.ctrl);
             if (e == hipSuccess) break;
             free_queues(ctx);
             (void)hipGetLastError();
@@ -985,128 +973,63 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         if (R.subs) Rc.subs = R.subs + c0;
         Rc.beam = beam;
         const uint32_t chunk_items = (uint32_t)((uint64_t)Rc.spp_count * n_px);
-        // the wavefront lanes: lane l runs its share of the chunk's items on stream ls[l]
-        // with its own half of the queues (BL[l]) and its own counter block; one lane for chunks too small
-        // to split
-        const uint32_t nl = (ctx->lanes == 2 && chunk_items >= 2u * kSegs * 64u) ? 2u : 1u;
-        const hipStream_t ls[2] = {s, nl == 2 ? ctx->lane_stream : s};
-        WaveBuffers BL[2] = {B, B};
-        DevRender RL[2] = {Rc, Rc};
-        uint32_t items_l[2] = {chunk_items, 0u}, n_seed_l[2] = {0u, 0u};
-        bool regen_l[2] = {false, false};
-        int grid_shade_l[2] = {0, 0};
-        if (nl == 2) {
-            items_l[0] = chunk_items / 2u;
-            items_l[1] = chunk_items - items_l[0];
-        }
-        const uint32_t pool_l = (uint32_t)(pool / nl);
-        for (uint32_t l = 0; l < nl; ++l) {
-            if (nl == 2) {
-                const uint32_t cap = B.seg_cap / 2u;
-                const size_t off = (size_t)l * kSegs * cap;
-                BL[l].seg_cap = cap;
-                for (int qq = 0; qq < 2; ++qq) {
-                    BL[l].ray0[qq] += off;
-                    BL[l].ray1[qq] += off;
-                }
-                BL[l].hit += off;
-                if (BL[l].huv) BL[l].huv += off;
-                BL[l].ctrl += (size_t)l * kCtrlWords;
-                RL[l].item_base = l * items_l[0];
-                RL[l].slot_base = l * pool_l;
-            }
-            // every item of the lane seeded at once (item = slot) when the pool holds the chunk, else
-            // the lane's share of the pool regenerates
-            n_seed_l[l] = pool >= chunk_items ? items_l[l] : std::min(pool_l, items_l[l]);
-            regen_l[l] = n_seed_l[l] < items_l[l];
-            // the lean 24-B path state: L stays 0 until the path ends, item = slot
-            BL[l].lean = (!regen_l[l] && ctx->lean_scene && !ctx->no_lean) ? 1u : 0u;
-            const int gs = grid_shade_of(shade_mode(regen_l[l], BL[l].lean != 0u));
-            // (a lane's shade: half the grid, still a multiple of kSegs waves)
-            grid_shade_l[l] = nl == 1 ? gs : ((gs / 2 + seg_blocks - 1) / seg_blocks) * seg_blocks;
-        }
-        ctx->wb.lean = BL[0].lean;
-        const int grid_ext_l = (nl == 1 || ctx->lane_full_grid) ? grid_extend : std::max(1, grid_extend / 2);
-        HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, nl * kCtrlWords * sizeof(uint32_t), s));
-        for (uint32_t l = 0; l < nl; ++l)
-            HIP_TRY(ctx, launch_wf_seed(ctx->C, RL[l], BL[l], n_seed_l[l], items_l[l], ctx->d_stats, s));
-        {
-        if (nl == 2) {
-            HIP_TRY(ctx, hipEventRecord(ctx->fork_ev, s));
-            HIP_TRY(ctx, hipStreamWaitEvent(ctx->lane_stream, ctx->fork_ev, 0));
-        }
-        // every exit from this block (the end, a cancel, a launch error) orders lane 1's work before the
-        // caller's stream's next
-        struct Join {
-            octpt_ctx *c;
-            hipStream_t s;
-            bool on;
-            ~Join() {
-                if (on && hipEventRecord(c->join_ev, c->lane_stream) == hipSuccess) (void)hipStreamWaitEvent(s, c->join_ev, 0);
-            }
-        } join{ctx, s, nl == 2};
-        uint32_t lane_it[2] = {0u, 0u};
-        bool lane_done[2] = {false, nl < 2};
-        while (!(lane_done[0] && lane_done[1])) {
-            for (uint32_t l = 0; l < nl; ++l) {
-                if (lane_done[l]) continue;
-                if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
-                const hipStream_t sl = ls[l];
-                const WaveBuffers &Bl = BL[l];
-                const uint32_t it = lane_it[l]++;
-                const uint32_t q = it & 1u;
-                EventPair ev{};
-                if ((st = ktimer_begin(ctx, sl, ev)) != OCTPT_OK) return st;
-                HIP_TRY(ctx, launch_wf_extend(ctx->S, Bl, q, ctx->refill, grid_ext_l, ctx->d_stats, sl));
-                if ((st = ktimer_end(ctx, sl, 0, ev)) != OCTPT_OK) return st;
-                if ((st = ktimer_begin(ctx, sl, ev)) != OCTPT_OK) return st;
-                HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, RL[l], Bl, q, items_l[l], it == 0u, regen_l[l], grid_shade_l[l],
-                                             ctx->d_stats, sl));
-                if ((st = ktimer_end(ctx, sl, 1, ev)) != OCTPT_OK) return st;
-                // snapshot of the queue iteration `it` produced; the host checks the snapshot of
-                // iteration it - kLookahead, so the GPU always has kLookahead iterations queued (an
-                // iteration over an empty queue exits at once).  The queue only empties once every
-                // chunk item is claimed: finished paths regenerate in the same shade pass.
-                const uint32_t slot = it % (kLookahead + 1);
-                uint32_t *hs = ctx->h_count + (l * (kLookahead + 1) + slot) * kCountSpan;
-                HIP_TRY(ctx, hipMemcpy2DAsync(hs, sizeof(uint32_t), Bl.ctrl + ctr_count(q ^ 1u, 0), kCtrStride * sizeof(uint32_t),
-                                              sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, sl));
-                HIP_TRY(ctx, hipMemcpy2DAsync(hs + kSegs, sizeof(uint32_t), Bl.ctrl + ctr_item(0), kCtrStride * sizeof(uint32_t),
-                                              sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, sl));
-                HIP_TRY(ctx, hipEventRecord(ctx->count_ev[l][slot], sl));
-                if (it < kLookahead) continue;
+        HIP_TRY(ctx, hipMemsetAsync(B.ctrl, 0, kCtrlWords * sizeof(uint32_t), s));
+        const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
+        const bool regen = n_seed < chunk_items;  // else the seed claimed every item of the chunk
+        // the lean 24-B path state: L stays 0 until the path ends, item = slot
+        ctx->wb.lean = (!regen && ctx->lean_scene && !ctx->no_lean) ? 1u : 0u;
+        const int grid_shade = grid_shade_of(shade_mode(regen, ctx->wb.lean != 0u));
+        HIP_TRY(ctx, launch_wf_seed(ctx->C, Rc, B, n_seed, chunk_items, ctx->d_stats, s));
+        for (uint32_t it = 0;; ++it) {
+            if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
+            const uint32_t q = it & 1u;
+            EventPair ev{};
+            if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
+            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, grid_extend, ctx->d_stats, s));
+            if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
+            if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
+            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, it == 0u, regen, grid_shade, ctx->d_stats, s));
+            if ((st = ktimer_end(ctx, s, 1, ev)) != OCTPT_OK) return st;
+            // snapshot of the queue iteration `it` produced; the host checks the snapshot of
+            // iteration it - kLookahead, so the GPU always has kLookahead iterations queued (an
+            // iteration over an empty queue exits at once).  The queue only empties once every
+            // chunk item is claimed: finished paths regenerate in the same shade pass.
+            const uint32_t slot = it % (kLookahead + 1);
+            uint32_t *hs = ctx->h_count + slot * kCountSpan;
+            HIP_TRY(ctx, hipMemcpy2DAsync(hs, sizeof(uint32_t), B.ctrl + ctr_count(q ^ 1u, 0), kCtrStride * sizeof(uint32_t),
+                                          sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, s));
+            HIP_TRY(ctx, hipMemcpy2DAsync(hs + kSegs, sizeof(uint32_t), B.ctrl + ctr_item(0), kCtrStride * sizeof(uint32_t),
+                                          sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, s));
+            HIP_TRY(ctx, hipEventRecord(ctx->count_ev[slot], s));
+            if (it >= kLookahead) {
                 const uint32_t old = (it - kLookahead) % (kLookahead + 1);
-                HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[l][old]));
-                const uint32_t *h = ctx->h_count + (l * (kLookahead + 1) + old) * kCountSpan;  // that iteration's queue, items
+                HIP_TRY(ctx, hipEventSynchronize(ctx->count_ev[old]));
+                const uint32_t *h = ctx->h_count + old * kCountSpan;  // that iteration's shade's queue, items
                 uint64_t queued = 0;
                 for (uint32_t k = 0; k < kSegs; ++k) queued += h[k];
-                if (queued == 0u) {  // iteration it - kLookahead + 1 onwards had nothing to do
-                    lane_done[l] = true;
-                    continue;
-                }
+                if (queued == 0u) break;  // iteration it - kLookahead + 1 onwards had nothing to do
                 // Drain: every chunk item claimed and few rays left, so the queue only shrinks from
                 // here (a ray yields at most one ray, and nothing regenerates).  One launch finishes the
                 // paths in the queue this iteration's shade filled instead of the launch-latency-bound
                 // tail of near-empty iterations.  Not in the extend timer (rocprof reports it as
                 // wf_drain_kernel); its statistics (<= 4096 paths) stay in the totals.
                 // (not for block-model scenes: their tails are transparent-texel chains, C5 -1 %)
-                if (queued <= ctx->drain_rays / nl && (!ctx->S.has_models || ctx->drain_models)) {
+                if (queued <= ctx->drain_rays && (!ctx->S.has_models || ctx->drain_models)) {
                     bool exhausted = true;
                     for (uint32_t k = 0; k < kSegs && exhausted; ++k) {
-                        const uint32_t lo = (uint32_t)(((uint64_t)k * items_l[l]) / kSegs);
-                        const uint32_t hi = (uint32_t)(((uint64_t)(k + 1u) * items_l[l]) / kSegs);
+                        const uint32_t lo = (uint32_t)(((uint64_t)k * chunk_items) / kSegs);
+                        const uint32_t hi = (uint32_t)(((uint64_t)(k + 1u) * chunk_items) / kSegs);
                         exhausted = h[kSegs + k] >= hi - lo;
                     }
                     if (exhausted) {
                         // one path per wave (wf_drain_kernel), four waves per block
-                        const int grid = (int)std::min<uint64_t>((queued + 3) / 4 + 1, (uint64_t)ctx->num_cu * 16u / nl);
-                        HIP_TRY(ctx, launch_wf_drain(ctx->S, RL[l], Bl, q ^ 1u, grid, ctx->d_stats, sl));
-                        lane_done[l] = true;
+                        const int grid = (int)std::min<uint64_t>((queued + 3) / 4 + 1, (uint64_t)ctx->num_cu * 16u);
+                        HIP_TRY(ctx, launch_wf_drain(ctx->S, Rc, B, q ^ 1u, grid, ctx->d_stats, s));
+                        break;
                     }
                 }
             }
         }
-        }  // lane 1 joined (Join)
         HIP_TRY(ctx, launch_wf_resolve(Rc, B, Rc.spp_count, d_accum, d_seg, s));
     }
     return OCTPT_OK;
@@ -1452,14 +1375,6 @@ octpt_status octpt_create(int32_t device, octpt_ctx **out) {
     ctx->mem_limit = (size_t)env_u32("OCTPT_DEVICE_MEM_LIMIT", 0u) << 20;  // MiB, test hook (ensure_wave)
     if (hipSetDevice(device) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
-    ctx->lanes = std::min<uint32_t>(env_u32("OCTPT_LANES", 1u), 2u);
-    const char *lane_grid_env = std::getenv("OCTPT_LANE_GRID");
-    ctx->lane_full_grid = lane_grid_env && std::strcmp(lane_grid_env, "full") == 0;
-    if (ctx->lanes == 2) {
-        if (hipStreamCreateWithFlags(&ctx->lane_stream, hipStreamNonBlocking) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
-        if (hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
-        if (hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
-    }
     if (hipMalloc(&ctx->d_counters, kCounterRing * sizeof(uint32_t)) != hipSuccess) return bail(OCTPT_ERR_OOM);
     if (hipMalloc(&ctx->d_stats, kStatWords * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_OOM);
     if (hipMemset(ctx->d_stats, 0, kStatWords * sizeof(unsigned long long)) != hipSuccess) return bail(OCTPT_ERR_DEVICE);
@@ -1543,13 +1458,8 @@ void octpt_destroy(octpt_ctx *ctx) {
     free_wave(ctx);
     ctx->build_scratch.release();
     if (ctx->h_count) (void)hipHostFree(ctx->h_count);
-    for (auto &lane : ctx->count_ev)
-        for (auto &ev : lane)
-            if (ev) (void)hipEventDestroy(ev);
-    if (ctx->lane_stream) (void)hipStreamSynchronize(ctx->lane_stream);
-    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
-    if (ctx->join_ev) (void)hipEventDestroy(ctx->join_ev);
-    if (ctx->lane_stream) (void)hipStreamDestroy(ctx->lane_stream);
+    for (auto &ev : ctx->count_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_subs) (void)hipFree(ctx->d_subs);
     if (ctx->d_beam) (void)hipFree(ctx->d_beam);

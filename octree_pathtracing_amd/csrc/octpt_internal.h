@@ -143,9 +143,6 @@ struct DevRender {
     // row), NULL = off (beam_kernel)
     const float *beam;
     uint32_t beam_tx;
-    // a wavefront lane's chunk items are [item_base, item_base + its chunk_items) of the chunk and its
-    // regenerating slots start at slot_base (OCTPT_LANES=2); 0 with one lane
-    uint32_t item_base, slot_base;
 };
 
 // TileRenderer::get_current_branch_count (tile_renderer.rs:196-206)

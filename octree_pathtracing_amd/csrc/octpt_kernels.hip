@@ -1973,7 +1973,7 @@ __device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveB
         bool dry = false;
         if (need) {
             if (t >= n) dry = true;
-            else if (seed_item<kSeed>(C, R, B, slot, R.item_base + lo + t, ps, cnt)) { ok = true; need = false; }
+            else if (seed_item<kSeed>(C, R, B, slot, lo + t, ps, cnt)) { ok = true; need = false; }
         }
         if (__ballot(dry) != 0ull) {
             const uint32_t j = threadIdx.x & 63u;
@@ -1986,7 +1986,6 @@ __device__ inline bool regen(const DevCamera &C, const DevRender &R, const WaveB
     return ok;
 }
 
-// (items and slots are offset by R.item_base / R.slot_base: a wavefront lane's)
 // seed: wave w appends to queue 0 segment w % kSegs, which holds at most seg_cap rays
 // (seg_cap = ceil(ceil(pool / 64) / kSegs) * 64).  When the pool holds the whole chunk
 // (n_seed == chunk_items: C3's frame, every 4K chunk) the waves of segment k take shard k's items
@@ -2007,12 +2006,11 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
         if (blockIdx.x == 0u && threadIdx.x < kSegs)
             B.ctrl[ctr_item(threadIdx.x)] = shard_lo(threadIdx.x + 1u, chunk_items) - shard_lo(threadIdx.x, chunk_items);
         const uint32_t item = shard_lo(seg, chunk_items) + (i >> 6) / kSegs * 64u + (i & 63u);
-        slot = R.item_base + item;
-        if (item < shard_lo(seg + 1u, chunk_items)) ok = seed_item<true>(C, R, B, slot, slot, ps, cnt);
+        slot = item;
+        if (item < shard_lo(seg + 1u, chunk_items)) ok = seed_item<true>(C, R, B, slot, item, ps, cnt);
     } else {
         ItemCursor cur = {seg, true};
-        slot = R.slot_base + i;
-        ok = regen<true>(C, R, B, slot, i < n_seed, chunk_items, cur, ps, cnt);
+        ok = regen<true>(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
     }
     const uint32_t t = wave_ticket(B.ctrl + ctr_count(0u, seg), ok);
     if (ok) store_ray(B, 0u, seg * B.seg_cap + t, slot, ps);

@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-r04l}
 mkdir -p $O
 cd $R
-OCTPT_LANES=2 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_lean.py tests/test_gpu_drain.py \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_lanes.py \
     -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_lanes_subset.txt 2>&1 \
     || { tail -40 $O/pytest_lanes_subset.txt; exit 1; }
 tail -3 $O/pytest_lanes_subset.txt
