@@ -117,6 +117,7 @@ struct octpt_ctx {
     uint64_t wave_allocs_n = 0;  // successful (re)allocations of the queues + path state
     bool oom_warned = false;
     uint32_t *h_count = nullptr;  // pinned ring: the segment counters after each iteration's shade
+    uint32_t *d_count = nullptr;  // its device address (wf_snapshot_kernel)
     hipEvent_t count_ev[kLookahead + 1] = {};
     uint32_t pool_cap = kDefaultPool, refill = kDefaultRefill;
     bool beam = true;  // camera rays start at their tile's beam (OCTPT_BEAM=0: off)
@@ -757,8 +758,10 @@ enum OomPart { kOomNone = 0, kOomQueues, kOomColor, kOomNee };
 octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool nee, bool blocks, OomPart *part) {
     *part = kOomNone;
     if (!ctx->h_count) {
+        // coherent (fine-grained) pinned memory: wf_snapshot_kernel's stores reach the host directly
         HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_count), (kLookahead + 1) * kCountSpan * sizeof(uint32_t),
-                                   hipHostMallocDefault));
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(ctx, hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_count), ctx->h_count, 0));
         for (auto &ev : ctx->count_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     }
     if (pool > ctx->pool) {
@@ -995,11 +998,15 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             // iteration over an empty queue exits at once).  The queue only empties once every
             // chunk item is claimed: finished paths regenerate in the same shade pass.
             const uint32_t slot = it % (kLookahead + 1);
+#ifdef OCTPT_SNAPSHOT_MEMCPY  // (A/B build: the two strided copies the snapshot kernel replaced)
             uint32_t *hs = ctx->h_count + slot * kCountSpan;
             HIP_TRY(ctx, hipMemcpy2DAsync(hs, sizeof(uint32_t), B.ctrl + ctr_count(q ^ 1u, 0), kCtrStride * sizeof(uint32_t),
                                           sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, s));
             HIP_TRY(ctx, hipMemcpy2DAsync(hs + kSegs, sizeof(uint32_t), B.ctrl + ctr_item(0), kCtrStride * sizeof(uint32_t),
                                           sizeof(uint32_t), kSegs, hipMemcpyDeviceToHost, s));
+#else
+            HIP_TRY(ctx, launch_wf_snapshot(B, q ^ 1u, ctx->d_count + slot * kCountSpan, s));
+#endif
             HIP_TRY(ctx, hipEventRecord(ctx->count_ev[slot], s));
             if (it >= kLookahead) {
                 const uint32_t old = (it - kLookahead) % (kLookahead + 1);

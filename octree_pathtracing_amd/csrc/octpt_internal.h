@@ -265,6 +265,9 @@ bool shade_lds_tables(const DevScene &S);
 // the drain of a chunk's last queued rays (every chunk item claimed): one launch, paths finished in-lane
 hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuffers &B, uint32_t q, int grid,
                            unsigned long long *stats, hipStream_t stream);
+// the host's snapshot of an iteration's counters: queue q's kSegs segment counts, then the kSegs item
+// counters, written by one 128-thread block into pinned host memory (enqueue_wavefront's steering)
+hipError_t launch_wf_snapshot(const WaveBuffers &B, uint32_t q, uint32_t *host_out, hipStream_t stream);
 hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,
                              uint32_t *segcount, hipStream_t stream);
 int extend_blocks_per_cu(const DevScene &S);

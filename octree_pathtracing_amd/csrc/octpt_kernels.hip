@@ -2791,6 +2791,20 @@ hipError_t launch_wf_drain(const DevScene &S, const DevRender &R, const WaveBuff
     return hipGetLastError();
 }
 
+// The host steering's snapshot (enqueue_wavefront): thread t < kSegs copies segment t's count of queue q,
+// thread kSegs + t shard t's item counter, into pinned host memory -- one small launch in the stream
+// instead of two strided device-to-host copies per iteration.
+__global__ __launch_bounds__(2 * kSegs) void wf_snapshot_kernel(const uint32_t *__restrict__ ctrl, uint32_t q,
+                                                                uint32_t *__restrict__ host_out) {
+    const uint32_t t = threadIdx.x;
+    host_out[t] = ctrl[t < kSegs ? ctr_count(q, t) : ctr_item(t - kSegs)];
+}
+
+hipError_t launch_wf_snapshot(const WaveBuffers &B, uint32_t q, uint32_t *host_out, hipStream_t stream) {
+    hipLaunchKernelGGL(wf_snapshot_kernel, dim3(1), dim3(2 * kSegs), 0, stream, B.ctrl, q, host_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_wf_resolve(const DevRender &R, const WaveBuffers &B, uint32_t chunk_spp, float4 *accum,
                              uint32_t *segcount, hipStream_t stream) {
     hipLaunchKernelGGL(wf_resolve_kernel, dim3((R.total_items + kBlock - 1u) / kBlock), dim3(kBlock), 0, stream, R, B,
