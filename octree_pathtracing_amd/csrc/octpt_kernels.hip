@@ -2005,9 +2005,23 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
     if (n_seed == chunk_items) {
         if (blockIdx.x == 0u && threadIdx.x < kSegs)
             B.ctrl[ctr_item(threadIdx.x)] = shard_lo(threadIdx.x + 1u, chunk_items) - shard_lo(threadIdx.x, chunk_items);
-        const uint32_t item = shard_lo(seg, chunk_items) + (i >> 6) / kSegs * 64u + (i & 63u);
+        const uint32_t lo = shard_lo(seg, chunk_items), hi = shard_lo(seg + 1u, chunk_items);
+        const uint32_t item = lo + (i >> 6) / kSegs * 64u + (i & 63u);
         slot = item;
-        if (item < shard_lo(seg + 1u, chunk_items)) ok = seed_item<true>(C, R, B, slot, item, ps, cnt);
+        if (item < hi) ok = seed_item<true>(C, R, B, slot, item, ps, cnt);
+        // Every tile inside the image (W and H multiples of the 8x8 tile: C3's 1080p, the 4K frames): no
+        // item is dropped, so shard k's items fill segment k in item order -- position item - lo, the
+        // count set by block 0 -- without a queue ticket per wave (8.3 M atomics per C3 frame on 64
+        // counters, ~2 ms at their measured rate, tools/atomic_bench.hip)
+#ifndef OCTPT_SEED_TICKET  // (A/B build: every wave takes a queue ticket)
+        if (((R.W | R.H) & (kTile - 1u)) == 0u) {
+            if (blockIdx.x == 0u && threadIdx.x < kSegs)
+                B.ctrl[ctr_count(0u, threadIdx.x)] = shard_lo(threadIdx.x + 1u, chunk_items) - shard_lo(threadIdx.x, chunk_items);
+            if (ok) store_ray(B, 0u, seg * B.seg_cap + (item - lo), slot, ps);
+            flush_counters(cnt, stats);
+            return;
+        }
+#endif
     } else {
         ItemCursor cur = {seg, true};
         ok = regen<true>(C, R, B, i, i < n_seed, chunk_items, cur, ps, cnt);
