@@ -2515,6 +2515,10 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, const flo
 constexpr int kBeamLevels = 24;
 static_assert(kTile % kBeamTile == 0, "beam tiles nest in the 8x8 render tiles");
 constexpr uint32_t kBeamSub = (kTile / kBeamTile) * (kTile / kBeamTile);  // beam tiles per render tile
+// the walk's stack levels: octants lie at levels 0 .. depth - 1
+__host__ __device__ constexpr uint32_t beam_levels(uint32_t depth) {
+    return depth < 1u ? 1u : depth < (uint32_t)kBeamLevels ? depth : (uint32_t)kBeamLevels;
+}
 #ifndef OCTPT_BEAM_VISITS
 #define OCTPT_BEAM_VISITS (1u << 13)
 #endif
@@ -2591,11 +2595,16 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
     // (conservative: it holds all its leaves; 0 = walk down to the leaf cells)
     const float lod = kBeamLod * fmaxf(s1 - s0, t1 - t0) / sqrtf(vdot(F, F));
     float best = __builtin_inff();
-    // the walk's stack in LDS, [level][thread]: octant base, mask, children still to visit (in
-    // front-to-back order: bit k = child k ^ om) and the cell's low corner
-    __shared__ uint32_t st_base[kBeamLevels][64], st_mask[kBeamLevels][64], st_rem[kBeamLevels][64];
-    __shared__ float st_lx[kBeamLevels][64], st_ly[kBeamLevels][64], st_lz[kBeamLevels][64];
-    const uint32_t t = threadIdx.x;
+    // the walk's stack in LDS, [level][thread], for the scene's depth levels (launch_beam sizes it:
+    // 6 x depth x 64 x 4 B, 12 KB at depth 8, so that 10+ blocks share a CU instead of 4 at a fixed 24
+    // levels): octant base, mask, children still to visit (in front-to-back order: bit k = child k ^ om)
+    // and the cell's low corner
+    extern __shared__ uint32_t beam_lds[];
+    const uint32_t t = threadIdx.x, L = beam_levels(S.depth);
+    uint32_t *const st_base = beam_lds, *const st_mask = beam_lds + L * 64u, *const st_rem = beam_lds + 2u * L * 64u;
+    float *const st_lx = reinterpret_cast<float *>(beam_lds + 3u * L * 64u);
+    float *const st_ly = reinterpret_cast<float *>(beam_lds + 4u * L * 64u);
+    float *const st_lz = reinterpret_cast<float *>(beam_lds + 5u * L * 64u);
     auto order = [&](uint32_t m) {  // present children, permuted so that bit k = child k ^ om
         uint32_t pm = m & 0xFFu;
         if (om & 1u) pm = ((pm & 0x55u) << 1) | ((pm >> 1) & 0x55u);
@@ -2607,33 +2616,33 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
     uint32_t nodes = 1u;  // octants the walk entered (the root included)
     if (!exhausted && box(V(1.0f, 1.0f, 1.0f), 1.0f) >= 0.0f) {
         int lv = 0;
-        st_base[0][t] = S.root;
-        st_mask[0][t] = S.root_mask;
-        st_rem[0][t] = order(S.root_mask);
-        st_lx[0][t] = st_ly[0][t] = st_lz[0][t] = 1.0f;
+        st_base[t] = S.root;
+        st_mask[t] = S.root_mask;
+        st_rem[t] = order(S.root_mask);
+        st_lx[t] = st_ly[t] = st_lz[t] = 1.0f;
         uint32_t visits = 0u;
         while (lv >= 0) {
-            const uint32_t rem = st_rem[lv][t];
+            const uint32_t rem = st_rem[lv * 64 + t];
             if (rem == 0u) { --lv; continue; }
             if (++visits > kBeamVisits) { exhausted = true; break; }
-            st_rem[lv][t] = rem & (rem - 1u);
+            st_rem[lv * 64 + t] = rem & (rem - 1u);
             const uint32_t ci = (uint32_t)(__ffs(rem) - 1) ^ om;
-            const uint32_t m = st_mask[lv][t], kind = (m >> ci) & 0x101u;
+            const uint32_t m = st_mask[lv * 64 + t], kind = (m >> ci) & 0x101u;
             const float h = __uint_as_float((126u - (uint32_t)lv) << 23);  // 2^-(lv + 1)
-            const v3 lo = V(st_lx[lv][t] + ((ci & 1u) ? h : 0.0f), st_ly[lv][t] + ((ci & 2u) ? h : 0.0f),
-                            st_lz[lv][t] + ((ci & 4u) ? h : 0.0f));
+            const v3 lo = V(st_lx[lv * 64 + t] + ((ci & 1u) ? h : 0.0f), st_ly[lv * 64 + t] + ((ci & 2u) ? h : 0.0f),
+                            st_lz[lv * 64 + t] + ((ci & 4u) ? h : 0.0f));
             const float d = box(lo, h);
             if (d < 0.0f || d >= best) continue;
-            if (kind == 0x101u || lv + 1 >= kBeamLevels || h <= lod * d) { best = d; continue; }  // leaf / small cell
-            const uint2 slot = S.node_child[st_base[lv][t] + __popc(m & ((1u << ci) - 1u))];
+            if (kind == 0x101u || lv + 1 >= (int)L || h <= lod * d) { best = d; continue; }  // leaf / small cell
+            const uint2 slot = S.node_child[st_base[lv * 64 + t] + __popc(m & ((1u << ci) - 1u))];
             ++lv;
             ++nodes;
-            st_base[lv][t] = slot.x;
-            st_mask[lv][t] = slot.y;
-            st_rem[lv][t] = order(slot.y);
-            st_lx[lv][t] = lo.x;
-            st_ly[lv][t] = lo.y;
-            st_lz[lv][t] = lo.z;
+            st_base[lv * 64 + t] = slot.x;
+            st_mask[lv * 64 + t] = slot.y;
+            st_rem[lv * 64 + t] = order(slot.y);
+            st_lx[lv * 64 + t] = lo.x;
+            st_ly[lv * 64 + t] = lo.y;
+            st_lz[lv * 64 + t] = lo.z;
         }
     }
     beam[tile] = exhausted ? 0.0f : beam_pack(best * (1.0f - 0x1p-16f), nodes);
@@ -2838,7 +2847,8 @@ hipError_t launch_intersect(const DevScene &S0, const float *rays, const uint32_
 
 hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R, float *beam, hipStream_t stream) {
     const uint32_t n = R.shard_tiles * kBeamSub;  // the shard's render tiles' beam tiles
-    hipLaunchKernelGGL(beam_kernel, dim3((n + 63u) / 64u), dim3(64), 0, stream, S, C, R, n, beam);
+    const size_t lds = 6u * beam_levels(S.depth) * 64u * sizeof(uint32_t);
+    hipLaunchKernelGGL(beam_kernel, dim3((n + 63u) / 64u), dim3(64), lds, stream, S, C, R, n, beam);
     return hipGetLastError();
 }
 
