@@ -62,11 +62,21 @@ def extend_queue_bytes(st: dict) -> float:
     return 40.0 * extend_share(st)["segments"]
 
 
-def shade_bytes(st: dict) -> float:
-    """DESIGN.md §8, wf_shade_kernel per segment: ray record 32 + hit 8 + path state 40 read,
-    path state 40 + ray record 32 written; per shaded hit 16 (sphere) + 4 (material id) + 48
-    (material record); 4 B per texel; 16 B per finished path (colour record)."""
-    return (152.0 * st["segments"] + 68.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
+def lean_state(sc, st: dict) -> bool:
+    """Whether the renders ran with the lean 24-B path state: no emitter (with emitters
+    on), no sun sampling, the pool holding the chunk, OCTPT_LEAN not 0 -- octpt_scene_upload's lean_scene
+    and enqueue_wavefront's per-chunk rule."""
+    emissive = sc.emitters_enabled and any(m.emittance > 5e-8 for m in sc.materials)
+    return (not emissive and not sc.strategy.sun_sampling and st["pool_slots"] >= st["chunk_items"]
+            and os.environ.get("OCTPT_LEAN", "") != "0")
+
+
+def shade_bytes(st: dict, lean: bool = False) -> float:
+    """DESIGN.md §8, wf_shade_kernel per segment: ray record 32 + hit 8 + path state read, path state +
+    ray record 32 written (the path state 40 B, or 24 B in the lean state); per shaded hit 16 (sphere) +
+    4 (material id) + 48 (material record); 4 B per texel; 16 B per finished path (colour record)."""
+    per_seg = 40.0 + 2.0 * (24.0 if lean else 40.0) + 32.0
+    return (per_seg * st["segments"] + 68.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
 
 
 def load_traffic(config: str):
@@ -368,7 +378,8 @@ def main():
     achieved = bytes_per_launch / ext_s / 1e9 if ext_s > 0 else 0.0
     n_sh = max(st["shade_launches"], 1)
     sh_s = st["shade_ms"] / 1e3 / n_sh
-    sh_bytes = shade_bytes(st) / n_sh
+    lean = lean_state(sc, st)
+    sh_bytes = shade_bytes(st, lean) / n_sh
     traffic, traffic_src, l2_hit = load_traffic(args.config)
     out = {
         "metric": METRIC,
@@ -414,7 +425,8 @@ def main():
             "share_of_gpu_time": round(st["extend_ms"] / max(st["extend_ms"] + st["shade_ms"], 1e-9), 3),
             "shade": {"kernel": "wf_shade_kernel", "launches": st["shade_launches"],
                       "kernel_ms_avg": round(sh_s * 1e3, 4), "algorithmic_bytes_per_launch": int(sh_bytes),
-                      "achieved": round(sh_bytes / sh_s / 1e9, 1) if sh_s > 0 else 0.0},
+                      "achieved": round(sh_bytes / sh_s / 1e9, 1) if sh_s > 0 else 0.0,
+                      "path_state_bytes": 24 if lean else 40},
         },
         "stats_rank0": {k: v for k, v in st.items() if k != "kernel_ms"},
     }

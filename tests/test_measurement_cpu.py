@@ -66,10 +66,33 @@ def test_bench_byte_counts():
     assert bench.extend_bytes(st) == 8 * 1000 + 20 * 10 + 28 * 5
     assert bench.extend_queue_bytes(st) == 40 * 7
     assert bench.shade_bytes(st) == 152 * 7 + 68 * 3 + 4 * 2 + 16 * 4
+    assert bench.shade_bytes(st, lean=True) == 120 * 7 + 68 * 3 + 4 * 2 + 16 * 4  # the 24-B path state
     # the drain kernel's share (octpt_stats.drain) is not extend's
     st["drain"] = {"esvo_steps": 100, "sphere_tests": 1, "cuboid_tests": 0, "segments": 2}
     assert bench.extend_bytes(st) == 8 * 900 + 20 * 9 + 28 * 5
     assert bench.extend_queue_bytes(st) == 40 * 5
+
+
+def test_bench_lean_state_rule(monkeypatch):
+    """The bench's shade byte model follows the library's lean-state rule."""
+    import bench
+    from octree_pathtracing_amd import scene as S
+
+    sc, _, _ = S.make_config("tiny")
+    st = {"pool_slots": 100, "chunk_items": 100}
+    monkeypatch.delenv("OCTPT_LEAN", raising=False)
+    assert bench.lean_state(sc, st)
+    assert not bench.lean_state(sc, {"pool_slots": 99, "chunk_items": 100})  # regeneration: the 40-B state
+    monkeypatch.setenv("OCTPT_LEAN", "0")
+    assert not bench.lean_state(sc, st)
+    monkeypatch.delenv("OCTPT_LEAN")
+    sc.materials[1].emittance = 5.0
+    sc.emitters_enabled = True
+    assert not bench.lean_state(sc, st)
+    sc.emitters_enabled = False
+    assert bench.lean_state(sc, st)
+    S.with_sun_variant(sc, "fast")
+    assert sc.strategy.sun_sampling and not bench.lean_state(sc, st)
 
 
 def test_bench_loads_committed_traffic():
