@@ -71,6 +71,14 @@ __device__ __forceinline__ float vmax3(v3 a) { return fmx(fmx(a.x, a.y), a.z); }
 __device__ __forceinline__ float tmn(float a, float b) { return __builtin_fminf(a, b); }
 __device__ __forceinline__ float tmx(float a, float b) { return __builtin_fmaxf(a, b); }
 __device__ __forceinline__ float tmin3(v3 a) { return tmn(tmn(a.x, a.y), a.z); }
+// min of two NaN-free t-values one of which the compiler cannot prove canonical (a loop-carried or
+// LDS-loaded t_max): one v_min_f32, where the minNum lowering puts a v_max canonicalisation of that
+// operand first (the same instruction, so the same bits, for NaN-free operands)
+__device__ __forceinline__ float tmn_nc(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ float tmax3(v3 a) { return tmx(tmx(a.x, a.y), a.z); }
 __device__ __forceinline__ float signum_(float f) { return (__float_as_uint(f) >> 31) ? -1.0f : 1.0f; }
 
@@ -1029,7 +1037,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // :142-244.  Leaf (t_min >= 0) and descend (t_min <= min(t_max, tc_max)) lanes share one slot
     // load instruction: on CDNA4 a scattered load costs the vector-memory pipe per instruction.
     // (t_min <= tv_max implies the reference's t_min <= t_max for the descend.)
-    const float tv_max = tmn(E.t_max, tc_max);
+    const float tv_max = tmn_nc(E.t_max, tc_max);
     const bool take_leaf = (kind == 0x101u) & !stopped & (E.t_min <= E.t_max) & (E.t_min >= 0.0f);
     const bool descend = (kind == 0x001u) & !stopped & (E.t_min <= tv_max);
     uint2 slot = make_uint2(0u, 0u);
@@ -1103,7 +1111,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const uint32_t cidx2 = E.idx ^ E.mirror;
         const v3 tc2 = vsub(vmul(E.pos, E.t_coef), E.t_bias);
         const float tc2_max = tmin3(tc2);
-        const float tv2_max = tmn(E.t_max, tc2_max);
+        const float tv2_max = tmn_nc(E.t_max, tc2_max);
         const bool d2 = (((E.pmask >> cidx2) & 0x101u) == 0x001u) & !esvo_capped(E.iter) &
                         !(E.t_min > max_dst) & (E.t_min <= tv2_max);
 #ifdef OCTPT_PROFILE_LANES
