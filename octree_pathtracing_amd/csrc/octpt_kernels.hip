@@ -2098,10 +2098,13 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
     bool rays_left = true;  // wave-uniform: some segment may still hold unclaimed rays
     uint32_t segs_w = 0u;   // segments started by this wave
     Counters cnt = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    bool active = false;
+    // a lane is busy while E.idx holds a child index (0..7); kIdle marks an idle lane, so that the
+    // loop's ballot of the idle lanes is one compare, not a lane-mask bool materialised and compared back
+    constexpr uint32_t kIdle = 8u;
     uint32_t pos = 0u;
     TraceRay tr;
     Esvo E;
+    E.idx = kIdle;
     bool more = true;
     // chunked claims: the wave owns [c_next, c_end) of segment seg and holds one further claim in
     // flight (lane 0's atomic result, read only when the owned chunk runs out), so a refill hands
@@ -2113,7 +2116,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
         claim_v = __hip_atomic_fetch_add(B.ctrl + ctr_head(q, seg), kClaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     do {
         // refill: one scalar test per iteration
-        const bool idle = !active;
+        const bool idle = E.idx >= kIdle;
         const uint64_t im = __ballot(idle);
         if (rays_left && (uint32_t)__popcll(im) >= thr) {
             if (c_next >= c_end) {  // the owned chunk ran out: take the claim in flight
@@ -2148,7 +2151,6 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk, ray_beam(r0, r1));
                     cnt.steps -= E.iter;  // a beam start's bound of skipped iterations: executed ones are counted
-                    active = true;
                 }
             }
             const uint32_t took = min((uint32_t)__popcll(im), avail);
@@ -2167,11 +2169,11 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
         // inner loop: step until `thr` lanes are idle (every lane, once no ray is left); its only
         // per-iteration bookkeeping is one ballot, a popcount and a scalar branch
         const uint32_t stop_at = __builtin_amdgcn_readfirstlane(rays_left ? thr : 64u);  // keeps the loop scalar
-        if ((uint32_t)__popcll(__ballot(!active)) < stop_at) do {
+        if ((uint32_t)__popcll(__ballot(E.idx >= kIdle)) < stop_at) do {
 #ifdef OCTPT_PROFILE_LANES
-            prof_wave(cnt.p_iters, cnt.p_active, active);
+            prof_wave(cnt.p_iters, cnt.p_active, E.idx < kIdle);
 #endif
-            if (active) {
+            if (E.idx < kIdle) {
                 uint32_t prim = kPrimNone;
                 PrimHit h;
                 HIT_POISON(h);
@@ -2193,10 +2195,10 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                         B.hit[p] = rs == kStepHit ? hit_record(prim, h) : miss;
                     }
                     cnt.steps += E.iter;
-                    active = false;
+                    E.idx = kIdle;
                 }
             }
-        } while ((uint32_t)__popcll(__ballot(!active)) < stop_at);  // at the bottom: no phi copies
+        } while ((uint32_t)__popcll(__ballot(E.idx >= kIdle)) < stop_at);  // at the bottom: no phi copies
         more = rays_left;  // wave-uniform; every lane is idle when it is false
     } while (more);
     cnt.segs = (threadIdx.x & 63u) == 0u ? segs_w : 0u;  // flush_counters sums over the wave's lanes
