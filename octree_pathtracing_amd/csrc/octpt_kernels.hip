@@ -1040,7 +1040,10 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const float tv_max = tmn_nc(E.t_max, tc_max);
     const bool take_leaf = (kind == 0x101u) & !stopped & (E.t_min <= E.t_max) & (E.t_min >= 0.0f);
     const bool descend = (kind == 0x001u) & !stopped & (E.t_min <= tv_max);
-    uint2 slot = make_uint2(0u, 0u);
+    // (a lane that loads nothing never reads slot: an empty asm hands it whatever its registers hold
+    // instead of zeroing them, two v_mov per step)
+    uint2 slot;
+    asm("" : "=v"(slot.x), "=v"(slot.y));
     const uint32_t sidx = E.parent + __popc(E.pmask & ((1u << cidx) - 1u));
     if (take_leaf | descend) {
         slot = S.node_child[sidx];
@@ -2174,7 +2177,10 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
             prof_wave(cnt.p_iters, cnt.p_active, E.idx < kIdle);
 #endif
             if (E.idx < kIdle) {
+                // set by the leaf test on a hit, the only case that reads it: left unspecified (no v_mov per
+                // step), except in the block-model instance, whose allocation spills 4 B more without the init
                 uint32_t prim = kPrimNone;
+                if constexpr (kPrims != kPrimsModels) asm("" : "=v"(prim));
                 PrimHit h;
                 HIT_POISON(h);
                 const int rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
