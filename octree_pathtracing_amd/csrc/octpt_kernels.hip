@@ -1169,7 +1169,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         const uint32_t diff = ((step_mask & 1u) ? dx : 0u) | ((step_mask & 2u) ? dy : 0u) | ((step_mask & 4u) ? dz : 0u);
         // diff != 0: a stepped axis moved by scale_exp2, so its pos differs from pos + scale_exp2
         // (the reference's diff == 0 case, util.rs:121-133, cannot arise here)
-        const uint32_t scale_raw = 31u - (uint32_t)__clz(diff);
+        const uint32_t scale_raw = 31u - (uint32_t)__builtin_clz(diff);  // (diff != 0: no zero-input clamp)
         // escaping the root is a miss (:281-283); its lane finishes the block on a clamped scale
         // and reports the miss at the end, so the pop stays one branch level
         const bool esc = scale_raw >= OCTREE_MAX_SCALE;
@@ -1178,9 +1178,9 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         // a pop rises above the level it advanced at (the step's own bit, 2^(s-23) in pos's
         // mantissa, always differs, and the pop condition means a higher one does), so
         // scale > base = OCTREE_MAX_SCALE - depth and the entry is in the LDS stack (levels 1..)
-        const uint32_t base = OCTREE_MAX_SCALE - S.depth;
-        const uint2 e = stk.e[(scale - base - 1u) * kS];
-        const uint32_t em = stk.m[(scale - base - 1u) * kS];
+        const uint32_t base1 = OCTREE_MAX_SCALE + 1u - S.depth;  // base + 1, wave-uniform
+        const uint2 e = stk.e[(scale - base1) * kS];
+        const uint32_t em = stk.m[(scale - base1) * kS];
         E.parent = e.x;
         E.pmask = em;
         E.t_max = __uint_as_float(e.y);
