@@ -79,18 +79,49 @@ def shade_bytes(st: dict, lean: bool = False) -> float:
     return (per_seg * st["segments"] + 68.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
 
 
-def load_traffic(config: str):
-    """(bytes per extend launch, source description, L2 hit rate) from profiles/pmc_<config>.json, or Nones."""
-    p = ROOT / "profiles" / f"pmc_{config}.json"
+def pmc_name(config: str, world: int = 1) -> str:
+    """The committed PMC profile a line of `config` at `world` ranks may quote: profiles/pmc_<config>.json for
+    one GPU, profiles/pmc_<config>_n<N>.json (rank 0's shard of an N-way split, scripts/shard_step.py) else."""
+    return f"pmc_{config}.json" if world == 1 else f"pmc_{config}_n{world}.json"
+
+
+def load_traffic(config: str, world: int = 1):
+    """(bytes per extend launch, source description, L2 hit rate) from the profile pmc_name(config, world)
+    names, or (None, reason, None): a line at N ranks never quotes a profile taken at another N."""
+    name = pmc_name(config, world)
+    p = ROOT / "profiles" / name
     if p.exists():
         try:
             d = json.loads(p.read_text())
             ext = d.get("wf_extend_kernel", {})
-            return ext.get("bytes_per_launch"), f"profiles/pmc_{config}.json: {d.get('correction', '')}", \
+            return ext.get("bytes_per_launch"), f"profiles/{name}: {d.get('correction', '')}", \
                 ext.get("l2_hit_rate")
-        except Exception:
-            return None, None, None
-    return None, None, None
+        except Exception as e:
+            return None, f"profiles/{name} unreadable ({type(e).__name__})", None
+    return None, f"no PMC profile of {config} at {world} rank(s) (profiles/{name})", None
+
+
+def roofline_over_ranks(ranks: list) -> dict:
+    """The extend roofline over N ranks (BASELINE.json's "achieved HBM GB/s vs roofline at 1/2/4/8 GPUs").
+    `ranks`: one dict per rank with `bytes` (algorithmic extend bytes of the timed steps, drain excluded),
+    `ext_ms` (the summed durations of its extend launches) and `launches`.  Rank r achieves
+    bytes_r / ext_ms_r; `achieved` is the per-GPU mean, `aggregate_gbs` = sum of the ranks' bytes / the
+    slowest rank's extend time, against `aggregate_peak` = N x the one-GPU peak; frac_min / frac_max give
+    the spread over ranks."""
+    per = []
+    for r in ranks:
+        t = r["ext_ms"] / 1e3
+        per.append(r["bytes"] / t / 1e9 if t > 0 else 0.0)
+    n = len(ranks)
+    tmax = max(r["ext_ms"] for r in ranks) / 1e3
+    agg = sum(r["bytes"] for r in ranks) / tmax / 1e9 if tmax > 0 else 0.0
+    mean = sum(per) / n
+    return {"achieved": round(mean, 1), "frac": round(mean / HBM_PEAK_GBS, 4),
+            "aggregate_gbs": round(agg, 1), "aggregate_peak": HBM_PEAK_GBS * n,
+            "aggregate_frac": round(agg / (HBM_PEAK_GBS * n), 4),
+            "frac_min": round(min(per) / HBM_PEAK_GBS, 4), "frac_max": round(max(per) / HBM_PEAK_GBS, 4),
+            "per_rank": [{"rank": i, "achieved": round(a, 1), "bytes": int(r["bytes"]), "ext_ms": round(r["ext_ms"], 3),
+                          "launches": int(r["launches"])} for i, (a, r) in enumerate(zip(per, ranks))]}
 
 
 def host_cpu() -> dict:
@@ -174,7 +205,7 @@ def issued_probe(sc, cam, rs, dev_idx: int, ext_s: float):
     if not lib.exists():
         return None
     import torch
-    from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
+    from octree_pathtracing_amd.renderer import HipRenderer, balance_tiles, shard_pixels
 
     r = HipRenderer(device=dev_idx, lib_path=str(lib))
     try:
@@ -244,6 +275,25 @@ def capi_multi_measure(sc, cam, rs, devices, steps: int, warmup: int) -> dict:
             "path": "octpt_create_multi + octpt_render_device (one process, peer-copy gather inside liboctpt)"}
 
 
+def balance_deal(r, segbuf, n_local: int, W: int, H: int, rank: int, world: int, cdev, balance_tiles) -> str:
+    """The N-rank tile deal of the timed steps: every rank's per-tile segment counts of the last
+    warmup step (its compact shard, 64 pixels per tile, dealt round robin) go to every rank, and each rank sets
+    the same order octpt_balance_tiles derives from them -- the previous frame's cost, as a progressive renderer
+    has it.  Rank 0's unshard follows the order (the same context)."""
+    from octree_pathtracing_amd.distributed import dealt_tiles, gather_rank_values, tiles_xy
+
+    mine = segbuf[:n_local].cpu().numpy().view(np.uint32).reshape(-1, 64).sum(1, dtype=np.int64)
+    most = max(len(dealt_tiles(W, H, k, world)) for k in range(world))
+    rows = gather_rank_values(np.pad(mine, (0, most - len(mine))).tolist(), world, cdev)
+    tx, ty = tiles_xy(W, H)
+    img = np.zeros(W * H, np.uint32)  # each tile's cost at its first pixel: balance_tiles sums per tile
+    for k in range(world):
+        t = dealt_tiles(W, H, k, world)
+        img[(t // tx) * 8 * W + (t % tx) * 8] = np.asarray(rows[k][:len(t)], np.float64).astype(np.uint32)
+    r.set_tile_order(W, H, balance_tiles(W, H, world, img))
+    return "balanced: octpt_balance_tiles over the warmup step's per-tile segment counts"
+
+
 def scene_contents(sc) -> str:
     if sc.blocks is not None:  # block-value leaves (DESIGN.md C23)
         return f"{len(sc.cells)} voxel cells as block-value leaves ({len(sc.blocks)} block kinds)"
@@ -269,6 +319,9 @@ def main():
     ap.add_argument("--capi-devices", default=None,
                     help="one process, one multi-device context (octpt_create_multi) over N devices or a list of "
                          "HIP ids: the C-ABI path a Rust host calls (DESIGN.md §9); ids repeat on a one-GPU box")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="with N > 1 ranks, keep the round-robin tile deal instead of the order octpt_balance_tiles "
+                         "derives from the warmup step's per-tile segment counts (DESIGN.md §9)")
     ap.add_argument("--no-capi-multi", action="store_true",
                     help="with N > 1 ranks, skip rank 0's extra measurement of the same frame through one "
                          "multi-device context over the N devices")
@@ -303,8 +356,8 @@ def main():
         assert dist.get_world_size() == args.gpus
 
     from octree_pathtracing_amd import scene as S
-    from octree_pathtracing_amd.distributed import gather_frame
-    from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
+    from octree_pathtracing_amd.distributed import gather_frame, gather_rank_values
+    from octree_pathtracing_amd.renderer import HipRenderer, balance_tiles, shard_pixels
 
     sc, cam, rs = S.make_config(args.config, build=not args.compact)
     if args.compact:
@@ -340,16 +393,22 @@ def main():
             g = gbuf_dev
         r.unshard_device(W, H, world, g.data_ptr(), stride, frame.data_ptr(), stream)
 
-    def step():
+    balance = world > 1 and not args.no_balance and args.warmup > 0
+    segbuf = torch.zeros(stride, dtype=torch.int32, device=dev) if balance else None
+
+    def step(seg=None):
         stream = torch.cuda.current_stream().cuda_stream
-        r.render_device(params, accum.data_ptr(), None, stream)
+        r.render_device(params, accum.data_ptr(), seg.data_ptr() if seg is not None else None, stream)
         if world > 1:  # gather to rank 0 (RCCL over xGMI), then the unshard kernel on rank 0
             src = accum.cpu() if host_staged else accum
             gather_frame(src, gbuf, W, H, rank, world, unshard)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(segbuf if i == args.warmup - 1 else None)
     torch.cuda.synchronize()
+    deal = "round robin"
+    if balance:  # the warmup step's per-tile segments, all ranks' to every rank, then one order everywhere
+        deal = balance_deal(r, segbuf, n_local, W, H, rank, world, gdev, balance_tiles)
     r.reset_stats()
     if world > 1:
         dist.barrier()
@@ -363,24 +422,23 @@ def main():
     dt = time.perf_counter() - t0
     st = r.stats()
     seg = st["segments"]
-    if world > 1:
-        cdev = gdev  # collectives on the backend's device (gloo: host tensors)
-        t = torch.tensor([dt], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        s = torch.tensor([seg], dtype=torch.float64, device=cdev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        seg = int(s.item())
+    mine = [dt, float(seg), extend_bytes(st), st["extend_ms"], float(st["extend_launches"])]
+    if world > 1:  # every rank's figures to every rank (collectives on the backend's device; gloo: host)
+        rows = gather_rank_values(mine, world, gdev)
+        dt = max(r[0] for r in rows)
+        seg = int(sum(r[1] for r in rows))
+    else:
+        rows = [mine]
+    over = roofline_over_ranks([{"bytes": r[2], "ext_ms": r[3], "launches": r[4]} for r in rows])
 
     n_ext = max(st["extend_launches"], 1)
     ext_s = st["extend_ms"] / 1e3 / n_ext
     bytes_per_launch = extend_bytes(st) / n_ext  # drain work excluded (extend_share)
-    achieved = bytes_per_launch / ext_s / 1e9 if ext_s > 0 else 0.0
     n_sh = max(st["shade_launches"], 1)
     sh_s = st["shade_ms"] / 1e3 / n_sh
     lean = lean_state(sc, st)
     sh_bytes = shade_bytes(st, lean) / n_sh
-    traffic, traffic_src, l2_hit = load_traffic(args.config)
+    traffic, traffic_src, l2_hit = load_traffic(args.config, world)
     out = {
         "metric": METRIC,
         "value": round(seg / dt / 1e6, 2),
@@ -404,18 +462,20 @@ def main():
             "parallelism": ((f"tiles{world}" + ("-gloo" if host_staged else "")) if world > 1
                             else f"capi-multi{len(multi)}" if multi else "single"),
             "paths_per_step": W * H * rs.spp,
+            "tile_deal": deal if world > 1 else None,
             "segments_per_step": seg // max(args.steps, 1),
         },
         "roofline": {
             "bound": "hbm",
-            "achieved": round(achieved, 1),
+            "achieved": over["achieved"],
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac": over["frac"],
             "traffic": traffic,
             "traffic_source": traffic_src,
             "l2_hit_rate": l2_hit,
             "kernel": "wf_extend_kernel",
+            # rank 0's launches (at N > 1 the per-rank figures are in `ranks`, the aggregate beside)
             "launches": st["extend_launches"],
             "kernel_ms_avg": round(ext_s * 1e3, 4),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
@@ -430,6 +490,11 @@ def main():
         },
         "stats_rank0": {k: v for k, v in st.items() if k != "kernel_ms"},
     }
+    if world > 1:  # achieved = the per-GPU mean; the whole job's extend GB/s against N x the peak
+        out["roofline"].update({k: over[k] for k in ("aggregate_gbs", "aggregate_peak", "aggregate_frac", "frac_min",
+                                                     "frac_max")})
+        out["roofline"]["ranks"] = over["per_rank"]
+        out["roofline"]["achieved_basis"] = "mean over ranks of each rank's extend bytes / its extend time"
     if multi:
         out["config"]["capi_devices"] = multi
     if world > 1 and not args.no_capi_multi:

@@ -327,10 +327,28 @@ octpt_status octpt_unshard_device(octpt_ctx *ctx, uint32_t width, uint32_t heigh
 /* pixels a shard owns (its compact buffer length in pixels, tile-padded) */
 uint32_t octpt_shard_pixels(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count);
 
+/* The tile deal (round 5).  The reference splits a frame into threads^2 tiles handed to a
+ * thread pool (tile_renderer.rs:398-413); here a shard of N owns the 8x8 tiles at dealing positions
+ * s = shard_index + u * N (its local tile u).  By default position s is frame tile s (round robin).
+ * octpt_set_tile_order sets the frame tile at each position for width x height renders of this context
+ * (order: ceil(W/8) * ceil(H/8) entries, a permutation; NULL = round robin again): renders, the async
+ * frame, octpt_unshard_device and every entry of a multi-device context follow it, and a render of another
+ * size is refused (INVALID_ARG) while it is set.  Per-pixel RNG streams keep the image bit-identical under
+ * any order; the order only moves work between shards. */
+octpt_status octpt_set_tile_order(octpt_ctx *ctx, uint32_t width, uint32_t height, const uint32_t *order);
+/* A balanced order for shard_count shards from a previous render's per-pixel segment counts (seg_count:
+ * width * height, image order, e.g. octpt_render's seg_count output): a tile's cost is the sum of its
+ * pixels' counts; tiles go, most costly first, to the shard with the least cost so far among those with
+ * positions left (each keeps its round-robin number of tiles), then each shard's tiles in image order.
+ * Host-only, no context; writes `order` (as octpt_set_tile_order takes it). */
+octpt_status octpt_balance_tiles(uint32_t width, uint32_t height, uint32_t shard_count, const uint32_t *seg_count,
+                                 uint32_t *order);
+
 /* Batch closest-hit query = Scene::hit (scene/mod.rs:172-187) with the octree traversal
- * (octree_traversal.rs:54-302) restored.  rays: n*6 floats (origin, unit direction), host; every
- * component finite and each direction component |d| <= 2^126 (else INVALID_ARG: ESVO's 1 / -|d| is
- * exact in that range; components below 2^-23 are clamped to it as the reference does).
+ * (octree_traversal.rs:54-302) restored.  rays: n*6 floats (origin, unit direction), host.  ESVO's
+ * 1 / -|d| is exact for direction components up to 2^126 (components below 2^-23 are clamped to it as
+ * the reference does); a ray with a non-finite component or a direction component above 2^126 is
+ * reported as a miss, as the reference's Scene::hit reports it, and the rest of the batch is traced.
  * last_prim / last_normal (nullable): self-intersection key per ray.
  * Outputs (host): t (world, +inf on miss), prim (0xFFFFFFFF on miss; in a block-value scene, C23, the
  * block id, or 0x40000000 | quad for a block model's quad), normal n*3 (nullable), esvo steps (nullable). */

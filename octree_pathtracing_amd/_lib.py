@@ -214,6 +214,8 @@ SIGNATURES = {
     "octpt_tonemap_device": (_i32, [_vp, _vp, _vp, _u32, _vp]),
     "octpt_unshard_device": (_i32, [_vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp]),
     "octpt_shard_pixels": (_u32, [_u32, _u32, _u32, _u32]),
+    "octpt_set_tile_order": (_i32, [_vp, _u32, _u32, _vp]),
+    "octpt_balance_tiles": (_i32, [_u32, _u32, _u32, _vp, _vp]),
     "octpt_intersect": (_i32, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp]),
     "octpt_traversal_data": (_i32, [_vp, _u32, _u32, _u32, _vp, _f, _vp, _vp, _vp, _vp]),
     "octpt_get_stats": (_i32, [_vp, C.POINTER(Stats)]),

@@ -134,6 +134,11 @@ struct octpt_ctx {
     float4 *m_acc = nullptr;
     uint32_t *m_seg = nullptr;
     size_t m_acc_cap = 0, m_seg_cap = 0;
+    // the tile deal (octpt_set_tile_order): for order_w x order_h frames, dealing position -> frame tile and
+    // its inverse, on this context's device; empty = the round-robin deal
+    std::vector<uint32_t> h_order;
+    uint32_t order_w = 0, order_h = 0;
+    uint32_t *d_order = nullptr, *d_order_pos = nullptr;
 };
 
 struct octpt_frame {
@@ -652,6 +657,13 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     R.subs = nullptr;
     R.beam = nullptr;
     R.beam_tx = (p->width + kBeamTile - 1) / kBeamTile;
+    R.tile_order = nullptr;
+    if (!ctx->h_order.empty()) {  // a tile order applies to the frame size it was set for
+        if (p->width != ctx->order_w || p->height != ctx->order_h)
+            return fail(ctx, OCTPT_ERR_INVALID_ARG,
+                        "render size differs from the tile order's (octpt_set_tile_order; NULL resets it)");
+        R.tile_order = ctx->d_order;
+    }
     if (B > 1u && !(p->flags & OCTPT_RENDER_PREVIEW)) {
         // TileRenderer pass schedule (tile_renderer.rs:416-484, C20): the call covers whole passes
         if (p->flags & OCTPT_RENDER_MEGAKERNEL)
@@ -1424,16 +1436,27 @@ octpt_status octpt_create_multi(const int32_t *devices, uint32_t n, octpt_ctx **
             return st;
         }
         // direct peer access between the first device and every other one (xGMI); without it the peer
-        // copies still work, staged by the runtime
+        // copies still work, staged by the runtime.  A pair that cannot be enabled is not an error, but it is
+        // recorded: octpt_last_error then reads "note: peer access ..." 
+        std::string note;
+        auto enable = [&](int from, int to) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, from, to) != hipSuccess || !can) {
+                note += " " + std::to_string(from) + "->" + std::to_string(to) + ": no peer path";
+                return;
+            }
+            if (hipSetDevice(from) != hipSuccess) return;
+            const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                note += " " + std::to_string(from) + "->" + std::to_string(to) + ": " + hipGetErrorString(e);
+            (void)hipGetLastError();
+        };
         for (uint32_t i = 1; i < n; ++i) {
-            int a = 0, b = 0;
             if (devices[i] == devices[0]) continue;
-            if (hipDeviceCanAccessPeer(&a, devices[0], devices[i]) == hipSuccess && a && hipSetDevice(devices[0]) == hipSuccess)
-                (void)hipDeviceEnablePeerAccess(devices[i], 0);
-            if (hipDeviceCanAccessPeer(&b, devices[i], devices[0]) == hipSuccess && b && hipSetDevice(devices[i]) == hipSuccess)
-                (void)hipDeviceEnablePeerAccess(devices[0], 0);
-            (void)hipGetLastError();  // hipErrorPeerAccessAlreadyEnabled for a repeated pair
+            enable(devices[0], devices[i]);
+            enable(devices[i], devices[0]);
         }
+        if (!note.empty()) ctx->err = "note: peer access not enabled (copies staged by the runtime):" + note;
         *out = ctx;
         return OCTPT_OK;
     } catch (...) {
@@ -1470,6 +1493,8 @@ void octpt_destroy(octpt_ctx *ctx) {
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_subs) (void)hipFree(ctx->d_subs);
     if (ctx->d_beam) (void)hipFree(ctx->d_beam);
+    if (ctx->d_order) (void)hipFree(ctx->d_order);
+    if (ctx->d_order_pos) (void)hipFree(ctx->d_order_pos);
     if (ctx->m_acc) (void)hipFree(ctx->m_acc);
     if (ctx->m_seg) (void)hipFree(ctx->m_seg);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
@@ -1838,10 +1863,95 @@ octpt_status octpt_unshard_device(octpt_ctx *ctx, uint32_t W, uint32_t H, uint32
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
     if (!d_shards || !d_frame || N == 0 || W == 0 || H == 0) return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad unshard args");
     if (stride < octpt_shard_pixels(W, H, 0, N)) return fail(ctx, OCTPT_ERR_INVALID_ARG, "shard stride too small");
+    if (!ctx->h_order.empty() && (W != ctx->order_w || H != ctx->order_h))
+        return fail(ctx, OCTPT_ERR_INVALID_ARG, "frame size differs from the tile order's (octpt_set_tile_order)");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, launch_unshard(W, H, N, reinterpret_cast<const float4 *>(d_shards), stride,
-                                reinterpret_cast<float4 *>(d_frame), static_cast<hipStream_t>(stream)));
+    HIP_TRY(ctx, launch_unshard(W, H, N, ctx->h_order.empty() ? nullptr : ctx->d_order_pos,
+                                reinterpret_cast<const float4 *>(d_shards), stride, reinterpret_cast<float4 *>(d_frame),
+                                static_cast<hipStream_t>(stream)));
     return OCTPT_OK;
+}
+
+octpt_status octpt_set_tile_order(octpt_ctx *ctx, uint32_t width, uint32_t height, const uint32_t *order) {
+    if (!ctx) return OCTPT_ERR_INVALID_ARG;
+    join_inflight(ctx);
+    try {
+        for (octpt_ctx *c : ctx->sub) {  // every device entry deals the same way (its sub-shards nest in it)
+            const octpt_status st = octpt_set_tile_order(c, width, height, order);
+            if (st != OCTPT_OK) return fail(ctx, st, c->err);
+        }
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        if (!order) {
+            ctx->h_order.clear();
+            ctx->order_w = ctx->order_h = 0;
+            return OCTPT_OK;
+        }
+        if (width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
+            return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad resolution");
+        const uint32_t T = ((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
+        std::vector<uint32_t> pos(T, 0xFFFFFFFFu);
+        for (uint32_t s = 0; s < T; ++s) {
+            if (order[s] >= T || pos[order[s]] != 0xFFFFFFFFu)
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "tile order is not a permutation of the frame's tiles");
+            pos[order[s]] = s;
+        }
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // an earlier render may still read the tables
+        if (ctx->h_order.size() != T) {
+            if (ctx->d_order) (void)hipFree(ctx->d_order);
+            if (ctx->d_order_pos) (void)hipFree(ctx->d_order_pos);
+            ctx->d_order = ctx->d_order_pos = nullptr;
+            ctx->h_order.clear();
+            HIP_TRY(ctx, hipMalloc(&ctx->d_order, (size_t)T * 4));
+            HIP_TRY(ctx, hipMalloc(&ctx->d_order_pos, (size_t)T * 4));
+        }
+        HIP_TRY(ctx, hipMemcpy(ctx->d_order, order, (size_t)T * 4, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(ctx->d_order_pos, pos.data(), (size_t)T * 4, hipMemcpyHostToDevice));
+        ctx->h_order.assign(order, order + T);
+        ctx->order_w = width;
+        ctx->order_h = height;
+        return OCTPT_OK;
+    } catch (const std::bad_alloc &) {
+        return fail(ctx, OCTPT_ERR_OOM, "host allocation");
+    } catch (...) {
+        return fail(ctx, OCTPT_ERR_INTERNAL, "unexpected exception");
+    }
+}
+
+octpt_status octpt_balance_tiles(uint32_t width, uint32_t height, uint32_t shard_count, const uint32_t *seg_count,
+                                 uint32_t *order) {
+    if (!seg_count || !order || shard_count == 0 || width == 0 || height == 0 ||
+        (uint64_t)width * height >= (1ull << 31))
+        return OCTPT_ERR_INVALID_ARG;
+    try {
+        const uint32_t tx = (width + kTile - 1) / kTile, T = tx * ((height + kTile - 1) / kTile);
+        std::vector<uint64_t> cost(T, 0);
+        for (uint32_t y = 0; y < height; ++y)
+            for (uint32_t x = 0; x < width; ++x) cost[(y / kTile) * tx + x / kTile] += seg_count[(size_t)y * width + x];
+        // longest processing time first: tiles by cost (ties by index), each to the shard with the least work
+        // so far among those with positions left -- shard k keeps exactly its round-robin count of positions
+        std::vector<uint32_t> by(T);
+        for (uint32_t t = 0; t < T; ++t) by[t] = t;
+        std::stable_sort(by.begin(), by.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        const uint32_t N = shard_count;
+        std::vector<uint64_t> load(N, 0);
+        std::vector<std::vector<uint32_t>> mine(N);
+        for (uint32_t k = 0; k < N; ++k) mine[k].reserve(tiles_of_shard(T, k, N));
+        for (uint32_t t : by) {
+            uint32_t best = N;
+            for (uint32_t k = 0; k < N; ++k)
+                if (mine[k].size() < tiles_of_shard(T, k, N) && (best == N || load[k] < load[best])) best = k;
+            mine[best].push_back(t);
+            load[best] += cost[t];
+        }
+        // each shard's tiles in image order (the seed's coherence: neighbouring tiles trace side by side)
+        for (uint32_t k = 0; k < N; ++k) {
+            std::sort(mine[k].begin(), mine[k].end());
+            for (uint32_t u = 0; u < mine[k].size(); ++u) order[k + (size_t)u * N] = mine[k][u];
+        }
+        return OCTPT_OK;
+    } catch (...) {
+        return OCTPT_ERR_OOM;
+    }
 }
 
 octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *last_prim, const float *last_normal,
@@ -1856,14 +1966,23 @@ octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *
         return st == OCTPT_OK ? st : fail(ctx, st, ctx->sub[0]->err);
     }
     // esvo_begin's t_coef = 1 / -|d| comes from rcp_rn, exact for |d| in [2^-23, 2^126] (smaller
-    // components are clamped to 2^-23 first, octree_traversal.rs:86-93): every component finite and
-    // |d| <= 2^126, which any unit direction meets
+    // components are clamped to 2^-23 first, octree_traversal.rs:86-93): a ray with a non-finite
+    // component or a direction component |d| > 2^126 is outside that range.  The reference's Scene::hit
+    // takes any ray and reports such one as a miss (its comparisons with NaN t-values all fail), so it is
+    // reported as a miss here too -- t = +inf, prim = none, normal 0, 0 steps -- and the rest of the
+    // batch is traced as usual (the kernel sees a placeholder ray in its place).
+    std::vector<uint32_t> unsupported;
+    std::vector<float> clean;
     for (size_t i = 0; i < (size_t)n * 6; ++i) {
         const float v = rays[i];
-        if (!std::isfinite(v) || (i % 6 >= 3 && std::fabs(v) > 0x1p126f))
-            return fail(ctx, OCTPT_ERR_INVALID_ARG,
-                        "ray " + std::to_string(i / 6) + ": origin and direction must be finite, |direction| <= 2^126");
+        if (!std::isfinite(v) || (i % 6 >= 3 && std::fabs(v) > 0x1p126f)) {
+            if (clean.empty()) clean.assign(rays, rays + (size_t)n * 6);
+            const size_t r = i / 6;
+            if (unsupported.empty() || unsupported.back() != r) unsupported.push_back((uint32_t)r);
+            for (int k = 0; k < 6; ++k) clean[r * 6 + k] = k == 3 ? 1.0f : 0.0f;
+        }
     }
+    if (!clean.empty()) rays = clean.data();
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     float *d_rays = nullptr, *d_ln = nullptr, *d_t = nullptr, *d_n = nullptr;
     uint32_t *d_lp = nullptr, *d_p = nullptr, *d_s = nullptr;
@@ -1896,6 +2015,12 @@ octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *
     } while (0);
     cleanup();
     if (e != hipSuccess) return hip_fail(ctx, e, "intersect");
+    for (uint32_t r : unsupported) {
+        t[r] = INFINITY;
+        prim[r] = 0xFFFFFFFFu;
+        if (normal) normal[3 * (size_t)r] = normal[3 * (size_t)r + 1] = normal[3 * (size_t)r + 2] = 0.0f;
+        if (steps) steps[r] = 0u;
+    }
     return OCTPT_OK;
 }
 

@@ -143,7 +143,13 @@ struct DevRender {
     // row), NULL = off (beam_kernel)
     const float *beam;
     uint32_t beam_tx;
+    // the tile deal (octpt_set_tile_order): dealing position s -> frame tile, NULL = identity.  Shard k owns
+    // positions s = k + u * shard_count (its local tile u), whatever the order
+    const uint32_t *tile_order;
 };
+
+// frame tile at dealing position s (octpt_set_tile_order's permutation, or s itself)
+__host__ __device__ inline uint32_t dealt_tile(const uint32_t *order, uint32_t s) { return order ? order[s] : s; }
 
 // TileRenderer::get_current_branch_count (tile_renderer.rs:196-206)
 inline uint32_t current_branch_count(uint32_t current_spp, uint32_t scene_branch_count) {
@@ -229,14 +235,15 @@ static_assert(kStatBeamRestartWord >= kStatCount && kStatBeamRestartWord < 12, "
 // false for a pixel outside the image in a frame layout (never read or written).
 __host__ __device__ inline bool multi_slot(uint32_t W, uint32_t H, uint32_t tiles_x, uint32_t shard_index,
                                            uint32_t shard_count, bool compact, uint32_t n_dev, uint32_t stride,
-                                           uint32_t i, uint32_t &caller, uint32_t &staged) {
+                                           uint32_t i, uint32_t &caller, uint32_t &staged,
+                                           const uint32_t *order = nullptr) {
     const uint32_t u = i / 64u, k = i % 64u;
     staged = (u % n_dev) * stride + (u / n_dev) * 64u + k;
     if (compact) {
         caller = i;
         return true;
     }
-    const uint32_t t = shard_index + u * shard_count;
+    const uint32_t t = dealt_tile(order, shard_index + u * shard_count);
     const uint32_t x = (t % tiles_x) * kTile + k % kTile, y = (t / tiles_x) * kTile + k / kTile;
     if (x >= W || y >= H) return false;
     caller = y * W + x;
@@ -277,7 +284,7 @@ hipError_t launch_intersect(const DevScene &S, const float *rays, const uint32_t
 hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R, float *beam, hipStream_t stream);
 hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const uint8_t *lut_byte,
                           hipStream_t stream);
-hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards,
+hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const uint32_t *tile_pos, const float4 *shards,
                           uint32_t stride, float4 *frame, hipStream_t stream);
 // the caller's buffers (accum, and seg when not NULL) <-> the staged compact buffers of n_dev device
 // entries (multi_slot), to_stage = caller -> staging

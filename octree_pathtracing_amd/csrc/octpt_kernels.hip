@@ -201,13 +201,23 @@ struct TraceRay {
     bool self_inward;
 };
 
-// ESVO stack in LDS: (octant, t_max) + the octant's child mask, [slot][thread] rows
 // per-lane ESVO stack in LDS: entry (parent base, t_max) and 16-bit mask per scale, lanes
-// interleaved with stride kStride (the threads of the block that traverse)
+// interleaved with stride kStride (the threads of the block that traverse).  (A packed 9-B entry for a
+// seventh wave of the depth-11 instances lost, round 5: tools/rejected/packed_stack.patch.)
 template <uint32_t kStride>
 struct StackT {
     uint2 *e;
     uint16_t *m;
+    __device__ __forceinline__ void write(uint32_t slot, uint32_t node, float t, uint32_t mask) const {
+        e[slot * kStride] = make_uint2(node, __float_as_uint(t));
+        m[slot * kStride] = (uint16_t)mask;
+    }
+    __device__ __forceinline__ void read(uint32_t slot, uint32_t &node, float &t, uint32_t &mask) const {
+        const uint2 v = e[slot * kStride];
+        node = v.x;
+        mask = m[slot * kStride];
+        t = __uint_as_float(v.y);
+    }
 };
 using Stack = StackT<kBlock>;
 
@@ -335,7 +345,7 @@ __device__ __forceinline__ uint2 hit_record(uint32_t prim, const PrimHit &h) {
 // that let the lane keep the value it entered the step with (the block-leaf defect of round 3).
 #ifdef OCTPT_CHECK_HITS
 constexpr uint32_t kHitSentinel = 0x7FC0DEADu;  // a NaN payload no hit computation produces
-#define HIT_POISON(h) ((h).t = (h).u = (h).v = __uint_as_float(kHitSentinel), (h).f = kHitSentinel)
+#define HIT_POISON(prim, h) ((prim) = kPrimNone, (h).t = (h).u = (h).v = __uint_as_float(kHitSentinel), (h).f = kHitSentinel)
 template <int kPrims>
 __device__ __forceinline__ bool hit_unwritten(uint32_t prim, const PrimHit &h) {
     if (prim == kPrimNone) return true;
@@ -350,9 +360,25 @@ __device__ __forceinline__ bool hit_unwritten(uint32_t prim, const PrimHit &h) {
         if ((rs) == kStepHit && hit_unwritten<kP>((prim), (h)))                                                  \
             atomicAdd(&(stats)[((row_base) + blockIdx.x % kSegs) * kStatRow + kStatHitCheckWord], 1ull);           \
     } while (0)
+// The step's node slot is poisoned the same way (esvo_step): only the lanes that load a slot (descend, leaf)
+// may take its fields, so a sentinel in the traversal state after a step -- the parent octant's slot base or
+// its child mask, which every later step and the LDS stack carry on -- is a lane that read a slot it never
+// loaded.  No slot base or mask equals the sentinel (slot arrays are < 2^31 entries, masks < 2^16).
+// A lane caught with the sentinel is counted and its ray ends (the step cap: its next step loads nothing and
+// reports a miss), so that a defect the check exposes never turns into a load from the poisoned base.
+#define SLOT_CHECK(E, stats, row_base)                                                                           \
+    do {                                                                                                        \
+        if ((E).parent == kHitSentinel || (E).pmask == kHitSentinel) {                                           \
+            atomicAdd(&(stats)[((row_base) + blockIdx.x % kSegs) * kStatRow + kStatHitCheckWord], 1ull);           \
+            (E).parent = 0u;                                                                                    \
+            (E).pmask = 0u;                                                                                     \
+            (E).iter = OCTREE_MAX_STEPS;                                                                        \
+        }                                                                                                       \
+    } while (0)
 #else
-#define HIT_POISON(h) ((void)0)
+#define HIT_POISON(prim, h) ((void)0)
 #define HIT_CHECK(kP, rs, prim, h, stats, row_base) ((void)0)
+#define SLOT_CHECK(E, stats, row_base) ((void)0)
 #endif
 
 // Sphere::hit restated (sphere.rs:33-57) + root selection [C2].  The square root and divisions
@@ -781,8 +807,7 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
 // ---------------------------------------------------------------------------
 template <uint32_t kS>
 __device__ __forceinline__ void stk_write(const StackT<kS> &stk, uint32_t slot, uint32_t node, float t, uint32_t mask) {
-    stk.e[slot * kS] = make_uint2(node, __float_as_uint(t));
-    stk.m[slot * kS] = (uint16_t)mask;
+    stk.write(slot, node, t, mask);
 }
 
 template <uint32_t kS = kBlock>
@@ -1041,9 +1066,13 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const bool take_leaf = (kind == 0x101u) & !stopped & (E.t_min <= E.t_max) & (E.t_min >= 0.0f);
     const bool descend = (kind == 0x001u) & !stopped & (E.t_min <= tv_max);
     // (a lane that loads nothing never reads slot: an empty asm hands it whatever its registers hold
-    // instead of zeroing them, two v_mov per step)
+    // instead of zeroing them, two v_mov per step; the check build poisons it instead, SLOT_CHECK)
     uint2 slot;
+#ifdef OCTPT_CHECK_HITS
+    slot = make_uint2(kHitSentinel, kHitSentinel);
+#else
     asm("" : "=v"(slot.x), "=v"(slot.y));
+#endif
     const uint32_t sidx = E.parent + __popc(E.pmask & ((1u << cidx) - 1u));
     if (take_leaf | descend) {
         slot = S.node_child[sidx];
@@ -1096,8 +1125,15 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     const uint32_t slot_u = (__float_as_uint(E.scale_exp2) >> 23) - 128u + S.depth;
     if (descend & (tc_max < E.h)) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
     E.h = descend ? tc_max : E.h;
-    E.parent = descend ? slot.x : E.parent;  // (octant, its mask)
-    E.pmask = descend ? slot.y : E.pmask;
+#ifdef OCTPT_SLOT_LEAK_PROBE
+    // negative control of SLOT_CHECK (scripts/stale_hit_probe.py slotleak_check): a lane advancing past an
+    // absent child takes the slot it never loaded; the check build must count it
+    const bool take_slot = descend | ((kind == 0u) & !stopped);
+#else
+    const bool take_slot = descend;
+#endif
+    E.parent = take_slot ? slot.x : E.parent;  // (octant, its mask)
+    E.pmask = take_slot ? slot.y : E.pmask;
     E.scale_exp2 = descend ? half : E.scale_exp2;
     E.t_max = descend ? tv_max : E.t_max;
     E.t_min = descend ? E.t_min : tc_max;
@@ -1179,11 +1215,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         // mantissa, always differs, and the pop condition means a higher one does), so
         // scale > base = OCTREE_MAX_SCALE - depth and the entry is in the LDS stack (levels 1..)
         const uint32_t base1 = OCTREE_MAX_SCALE + 1u - S.depth;  // base + 1, wave-uniform
-        const uint2 e = stk.e[(scale - base1) * kS];
-        const uint32_t em = stk.m[(scale - base1) * kS];
-        E.parent = e.x;
-        E.pmask = em;
-        E.t_max = __uint_as_float(e.y);
+        stk.read(scale - base1, E.parent, E.t_max, E.pmask);
         // pos truncated to the popped scale; idx = pos bits at that scale
         const uint32_t keep = 0xFFFFFFFFu << scale;
         const uint32_t px = __float_as_uint(E.pos.x) & keep, py = __float_as_uint(E.pos.y) & keep,
@@ -1569,7 +1601,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 
 __device__ __forceinline__ void item_pixel(const DevRender &R, uint32_t item, uint32_t &x, uint32_t &y) {
     const uint32_t lt = item >> 6, w = item & 63u;
-    const uint32_t t = R.shard_index + lt * R.shard_count;
+    const uint32_t t = dealt_tile(R.tile_order, R.shard_index + lt * R.shard_count);
     x = (t % R.tiles_x) * kTile + (w & 7u);
     y = (t / R.tiles_x) * kTile + (w >> 3);
 }
@@ -2165,7 +2197,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 // (a lane's rays counted as the wave's average, segs_w / 64: no per-lane counter, which
                 // the block instance spilled to scratch at every refill)
                 // (signed: a lane's in-flight beam start has been subtracted already)
-                const bool short_rays = (int32_t)cnt.steps * 64 < (int32_t)(kShortRaySteps * segs_w);
+                const bool short_rays = (int64_t)(int32_t)cnt.steps * 64 < (int64_t)kShortRaySteps * segs_w;
                 thr = __popcll(__ballot(short_rays)) > 32 ? OCTPT_THR_SHORT : OCTPT_THR_LONG;
             }
         }
@@ -2179,11 +2211,15 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
             if (E.idx < kIdle) {
                 // set by the leaf test on a hit, the only case that reads it: left unspecified (no v_mov per
                 // step), except in the block-model instance, whose allocation spills 4 B more without the init
+                // (the check build keeps kPrimNone, so that a hit that never wrote its id is counted)
                 uint32_t prim = kPrimNone;
+#ifndef OCTPT_CHECK_HITS
                 if constexpr (kPrims != kPrimsModels) asm("" : "=v"(prim));
+#endif
                 PrimHit h;
-                HIT_POISON(h);
+                HIT_POISON(prim, h);
                 const int rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
+                SLOT_CHECK(E, stats, 0u);
                 if (rs != kStepContinue) {
                     HIT_CHECK(kPrims, rs, prim, h, stats, 0u);
                     // the record's address is formed here from pos (through an empty asm), not kept
@@ -2396,8 +2432,9 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                 int rs;
                 for (;;) {
                     do {
-                        HIT_POISON(h);
+                        HIT_POISON(prim, h);
                         rs = esvo_step<kPrims, true>(S, tr, E, stk, cnt, prim, h);
+                        SLOT_CHECK(E, stats, kStatDrainRow);
                     } while (rs == kStepContinue);
                     HIT_CHECK(kPrims, rs, prim, h, stats, kStatDrainRow);
                     cnt.steps += E.iter;
@@ -2560,13 +2597,131 @@ __device__ __forceinline__ float beam_pack(float t, uint32_t nodes) {
     return __uint_as_float(((b - (kBeamIterMask + 1u)) & ~kBeamIterMask) | bound);
 }
 
+#ifndef OCTPT_BEAM_COOP
+#define OCTPT_BEAM_COOP 1
+#endif
+#if OCTPT_BEAM_COOP
+// Round 5: kBeamLanes lanes per beam tile, lane j standing for child j of the octant the
+// walk is in.  Entering an octant tests its eight children's boxes at once (while its node slot is in flight),
+// and each iteration takes the nearest child still nearer than the best leaf so far (a min over the group's
+// eight lanes, three xor shuffles), so the walk's sequential length is the number of cells it takes, not the
+// number of children it tests; eight tiles share a 64-lane wave, and an 8-way shard's 16 K C3 tiles fill
+// 2 K waves instead of 253.  The start is the same distance (the minimum over the pyramid's leaf cells, by the
+// same box arithmetic), so only the walk's octant count -- the iteration bound it packs -- differs.
+constexpr uint32_t kBeamLanes = 8u;
+__global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRender R, uint32_t n_tiles,
+                                                  float *__restrict__ beam) {
+    const uint32_t lane = threadIdx.x & (kBeamLanes - 1u), grp = threadIdx.x / kBeamLanes;
+    // group g of block b: beam tile i = b * 8 + g, i.e. beam tile i % kBeamSub of the shard's render tile
+    // i / kBeamSub (item_pixel's tile order), so a rank of N computes only its own tiles' starts
+    const uint32_t i = blockIdx.x * (64u / kBeamLanes) + grp;
+    if (i >= n_tiles) return;  // whole groups leave: the shuffles below stay inside a group
+    const uint32_t rt = dealt_tile(R.tile_order, R.shard_index + (i / kBeamSub) * R.shard_count), sub = i % kBeamSub;
+    const uint32_t x0 = (rt % R.tiles_x) * kTile + (sub % (kTile / kBeamTile)) * kBeamTile,
+                   y0 = (rt / R.tiles_x) * kTile + (sub / (kTile / kBeamTile)) * kBeamTile;
+    if (x0 >= R.W || y0 >= R.H) return;  // no pixel of the image: never read
+    const uint32_t tile = (y0 / kBeamTile) * R.beam_tx + x0 / kBeamTile;
+    const uint32_t x1 = min(x0 + kBeamTile, R.W), y1 = min(y0 + kBeamTile, R.H);
+    // screen coordinates of the tile's rays (new_path: xn + dx, yn + dy), padded by 2 % + 1e-6
+    float s0 = ((float)(2u * x0) - (float)R.W) / R.dim, s1 = ((float)(2u * x1) - (float)R.W) / R.dim;
+    float t0 = ((float)(2u * (R.H - y1)) - (float)R.H) / R.dim, t1 = ((float)(2u * (R.H - y0)) - (float)R.H) / R.dim;
+    const float ps = 0.02f * (s1 - s0) + 1e-6f, pt = 0.02f * (t1 - t0) + 1e-6f;
+    s0 -= ps; s1 += ps; t0 -= pt; t1 += pt;
+    const v3 F = vscale(V(C.dir[0], C.dir[1], C.dir[2]), C.d_factor);
+    const v3 Rt = V(C.right[0], C.right[1], C.right[2]), Up = V(C.up[0], C.up[1], C.up[2]);
+    const v3 Ek[4] = {vadd(vadd(F, vscale(Rt, s0)), vscale(Up, t0)), vadd(vadd(F, vscale(Rt, s1)), vscale(Up, t0)),
+                      vadd(vadd(F, vscale(Rt, s1)), vscale(Up, t1)), vadd(vadd(F, vscale(Rt, s0)), vscale(Up, t1))};
+    const v3 Ec = vadd(vadd(F, vscale(Rt, 0.5f * (s0 + s1))), vscale(Up, 0.5f * (t0 + t1)));
+    v3 pn[4];
+    for (int k = 0; k < 4; ++k) {
+        v3 n = vcross(Ek[k], Ek[(k + 1) & 3]);
+        if (vdot(n, Ec) < 0.0f) n = vscale(n, -1.0f);
+        pn[k] = n;
+    }
+    // the eye as esvo_begin places a ray origin in octree space
+    const v3 e = vadd(vscale(V(C.eye[0], C.eye[1], C.eye[2]), S.octree_scale), V(1.0f, 1.0f, 1.0f));
+    // distance from the eye to the box [lo, lo + h], or -1 when the box lies outside the pyramid
+    auto box = [&](v3 lo, float h) -> float {
+        const v3 a = vsub(lo, e), b = vsub(vadd(lo, V(h, h, h)), e);
+        const float ext = fmaxf(fmaxf(fmaxf(fabsf(a.x), fabsf(b.x)), fmaxf(fabsf(a.y), fabsf(b.y))),
+                                fmaxf(fabsf(a.z), fabsf(b.z)));
+        for (int k = 0; k < 4; ++k) {
+            const v3 n = pn[k];
+            const float mx = (fmaxf(n.x * a.x, n.x * b.x) + fmaxf(n.y * a.y, n.y * b.y)) + fmaxf(n.z * a.z, n.z * b.z);
+            const float tol = 1e-5f * ((fabsf(n.x) + fabsf(n.y)) + fabsf(n.z)) * ext;
+            if (mx < -tol) return -1.0f;
+        }
+        const float dx = a.x > 0.0f ? a.x : (b.x < 0.0f ? -b.x : 0.0f);
+        const float dy = a.y > 0.0f ? a.y : (b.y < 0.0f ? -b.y : 0.0f);
+        const float dz = a.z > 0.0f ? a.z : (b.z < 0.0f ? -b.z : 0.0f);
+        return sqrtf((dx * dx + dy * dy) + dz * dz);
+    };
+    const float lod = kBeamLod * fmaxf(s1 - s0, t1 - t0) / sqrtf(vdot(F, F));
+    float best = __builtin_inff();
+    // LDS, for the scene's depth levels (launch_beam sizes it: (64 + 5 x 8) x depth x 4 B, 3.3 KB at depth 8):
+    // st_d[level][thread] = the distance of child `lane` of the level's octant (+inf: absent, outside the
+    // pyramid, or taken), and per group the octant's slot base, mask and low corner (every lane of the group
+    // writes the same value: no lane-0 branch)
+    extern __shared__ uint32_t beam_lds[];
+    const uint32_t t = threadIdx.x, L = beam_levels(S.depth);
+    constexpr uint32_t G = 64u / kBeamLanes;
+    float *const st_d = reinterpret_cast<float *>(beam_lds);
+    uint32_t *const st_base = beam_lds + L * 64u, *const st_mask = st_base + L * G;
+    float *const st_lx = reinterpret_cast<float *>(st_mask + L * G), *const st_ly = st_lx + L * G, *const st_lz = st_ly + L * G;
+    // child `lane` of the octant at `lo` (children of size hc) with mask m: its distance, or +inf
+    auto child_d = [&](v3 lo, float hc, uint32_t m) -> float {
+        const v3 clo = V(lo.x + ((lane & 1u) ? hc : 0.0f), lo.y + ((lane & 2u) ? hc : 0.0f), lo.z + ((lane & 4u) ? hc : 0.0f));
+        const float d = box(clo, hc);
+        return (((m >> lane) & 1u) != 0u && d >= 0.0f) ? d : __builtin_inff();
+    };
+    bool exhausted = S.depth >= (uint32_t)kBeamLevels;
+    uint32_t nodes = 1u;  // octants the walk entered (the root included)
+    if (!exhausted && box(V(1.0f, 1.0f, 1.0f), 1.0f) >= 0.0f) {
+        int lv = 0;
+        st_base[grp] = S.root;
+        st_mask[grp] = S.root_mask;
+        st_lx[grp] = st_ly[grp] = st_lz[grp] = 1.0f;
+        st_d[t] = child_d(V(1.0f, 1.0f, 1.0f), 0.5f, S.root_mask);
+        uint32_t visits = 0u;
+        while (lv >= 0) {  // group-uniform control flow: every decision below is the group's
+            const float dj = st_d[lv * 64 + t];
+            // the nearest child still nearer than best: its distance's bits (>= 0, so ordered as unsigned)
+            // with the lane in the low 3 bits, minimised over the group
+            uint32_t k = dj < best ? ((__float_as_uint(dj) & ~7u) | lane) : 0xFFFFFFFFu;
+            k = min(k, (uint32_t)__shfl_xor((int)k, 1, kBeamLanes));
+            k = min(k, (uint32_t)__shfl_xor((int)k, 2, kBeamLanes));
+            k = min(k, (uint32_t)__shfl_xor((int)k, 4, kBeamLanes));
+            if (k == 0xFFFFFFFFu) { --lv; continue; }
+            if (++visits > kBeamVisits) { exhausted = true; break; }
+            const uint32_t ci = k & 7u;
+            const float d = __shfl(dj, (int)ci, kBeamLanes);  // its exact distance
+            if (lane == ci) st_d[lv * 64 + t] = __builtin_inff();
+            const uint32_t m = st_mask[lv * G + grp], kind = (m >> ci) & 0x101u;
+            const float h = __uint_as_float((126u - (uint32_t)lv) << 23);  // 2^-(lv + 1)
+            if (kind == 0x101u || lv + 1 >= (int)L || h <= lod * d) { best = d; continue; }  // leaf / small cell
+            const uint2 slot = S.node_child[st_base[lv * G + grp] + __popc(m & ((1u << ci) - 1u))];
+            const v3 lo = V(st_lx[lv * G + grp] + ((ci & 1u) ? h : 0.0f), st_ly[lv * G + grp] + ((ci & 2u) ? h : 0.0f),
+                            st_lz[lv * G + grp] + ((ci & 4u) ? h : 0.0f));
+            ++lv;
+            ++nodes;
+            st_base[lv * G + grp] = slot.x;
+            st_mask[lv * G + grp] = slot.y;
+            st_lx[lv * G + grp] = lo.x;
+            st_ly[lv * G + grp] = lo.y;
+            st_lz[lv * G + grp] = lo.z;
+            st_d[lv * 64 + t] = child_d(lo, h * 0.5f, slot.y);
+        }
+    }
+    if (lane == 0u) beam[tile] = exhausted ? 0.0f : beam_pack(best * (1.0f - 0x1p-16f), nodes);
+}
+#else
 __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRender R, uint32_t n_tiles,
                                                   float *__restrict__ beam) {
     // thread i: beam tile i % kBeamSub of the shard's render tile i / kBeamSub (item_pixel's tile order),
     // so a rank of N computes only its own tiles' starts
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i >= n_tiles) return;
-    const uint32_t rt = R.shard_index + (i / kBeamSub) * R.shard_count, sub = i % kBeamSub;
+    const uint32_t rt = dealt_tile(R.tile_order, R.shard_index + (i / kBeamSub) * R.shard_count), sub = i % kBeamSub;
     const uint32_t x0 = (rt % R.tiles_x) * kTile + (sub % (kTile / kBeamTile)) * kBeamTile,
                    y0 = (rt / R.tiles_x) * kTile + (sub / (kTile / kBeamTile)) * kBeamTile;
     if (x0 >= R.W || y0 >= R.H) return;  // no pixel of the image: never read
@@ -2664,6 +2819,8 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
     beam[tile] = exhausted ? 0.0f : beam_pack(best * (1.0f - 0x1p-16f), nodes);
 }
 
+#endif
+
 __global__ void tonemap_kernel(const float4 *__restrict__ accum, uchar4 *__restrict__ out, uint32_t n,
                                const uint8_t *__restrict__ lut) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2674,13 +2831,14 @@ __global__ void tonemap_kernel(const float4 *__restrict__ accum, uchar4 *__restr
     out[i] = make_uchar4(lut[f2u32_sat(r)], lut[f2u32_sat(g)], lut[f2u32_sat(b)], (uint8_t)f2u32_sat(a));
 }
 
-__global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t N, const float4 *__restrict__ shards, uint32_t stride,
-                               float4 *__restrict__ frame) {
+// tile_pos (nullable): frame tile -> dealing position, the inverse of the tile order (octpt_set_tile_order)
+__global__ void unshard_kernel(uint32_t W, uint32_t H, uint32_t N, const uint32_t *__restrict__ tile_pos,
+                               const float4 *__restrict__ shards, uint32_t stride, float4 *__restrict__ frame) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= W * H) return;
     const uint32_t x = i % W, y = i / W;
     const uint32_t tiles_x = (W + kTile - 1u) / kTile;
-    const uint32_t t = (y / kTile) * tiles_x + x / kTile;
+    const uint32_t t = dealt_tile(tile_pos, (y / kTile) * tiles_x + x / kTile);
     const uint32_t shard = t % N, lt = t / N;
     frame[i] = shards[(size_t)shard * stride + (size_t)lt * 64u + (y % kTile) * kTile + (x % kTile)];
 }
@@ -2692,7 +2850,9 @@ __global__ void multi_stage_kernel(DevRender R, uint32_t n_dev, uint32_t stride,
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R.total_items) return;
     uint32_t c, st;
-    if (!multi_slot(R.W, R.H, R.tiles_x, R.shard_index, R.shard_count, R.compact != 0u, n_dev, stride, i, c, st)) return;
+    if (!multi_slot(R.W, R.H, R.tiles_x, R.shard_index, R.shard_count, R.compact != 0u, n_dev, stride, i, c, st,
+                    R.tile_order))
+        return;
     if (to_stage) {
         stage_accum[st] = accum[c];
         if (seg) stage_seg[st] = seg[c];
@@ -2863,8 +3023,14 @@ hipError_t launch_intersect(const DevScene &S0, const float *rays, const uint32_
 
 hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R, float *beam, hipStream_t stream) {
     const uint32_t n = R.shard_tiles * kBeamSub;  // the shard's render tiles' beam tiles
+#if OCTPT_BEAM_COOP
+    const size_t lds = (64u + 5u * (64u / kBeamLanes)) * beam_levels(S.depth) * sizeof(uint32_t);
+    const uint32_t per_block = 64u / kBeamLanes;
+#else
     const size_t lds = 6u * beam_levels(S.depth) * 64u * sizeof(uint32_t);
-    hipLaunchKernelGGL(beam_kernel, dim3((n + 63u) / 64u), dim3(64), lds, stream, S, C, R, n, beam);
+    const uint32_t per_block = 64u;
+#endif
+    hipLaunchKernelGGL(beam_kernel, dim3((n + per_block - 1u) / per_block), dim3(64), lds, stream, S, C, R, n, beam);
     return hipGetLastError();
 }
 
@@ -2880,10 +3046,10 @@ hipError_t launch_multi_stage(const DevRender &R, uint32_t n_dev, uint32_t strid
     return hipGetLastError();
 }
 
-hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const float4 *shards, uint32_t stride,
-                          float4 *frame, hipStream_t stream) {
-    hipLaunchKernelGGL(unshard_kernel, dim3((W * H + 255u) / 256u), dim3(256), 0, stream, W, H, shard_count, shards,
-                       stride, frame);
+hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const uint32_t *tile_pos, const float4 *shards,
+                          uint32_t stride, float4 *frame, hipStream_t stream) {
+    hipLaunchKernelGGL(unshard_kernel, dim3((W * H + 255u) / 256u), dim3(256), 0, stream, W, H, shard_count, tile_pos,
+                       shards, stride, frame);
     return hipGetLastError();
 }
 

@@ -267,6 +267,15 @@ class HipRenderer:
         self._check(self._lib.octpt_unshard_device(self._ctx, W, H, shard_count, C.c_void_p(d_shards), stride,
                                                    C.c_void_p(d_frame), C.c_void_p(stream) if stream else None))
 
+    def set_tile_order(self, W: int, H: int, order: np.ndarray | None) -> None:
+        """The tile deal for W x H renders (octpt_set_tile_order): order[s] = the frame tile at dealing position s
+        (shard k owns positions k + u * N); None = round robin."""
+        if order is None:
+            self._check(self._lib.octpt_set_tile_order(self._ctx, W, H, None))
+            return
+        o = np.ascontiguousarray(order, np.uint32)
+        self._check(self._lib.octpt_set_tile_order(self._ctx, W, H, o.ctypes.data_as(C.c_void_p)))
+
     def intersect(self, rays: np.ndarray, last_prim=None, last_normal=None):
         """Batch Scene::hit: returns (t, prim, normal, steps)."""
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
@@ -312,3 +321,18 @@ def branch_pass_end(spp_start: int, spp_count: int, scene_branch_count: int) -> 
 
 def shard_pixels(W: int, H: int, shard_index: int, shard_count: int) -> int:
     return int(_lib.load().octpt_shard_pixels(W, H, shard_index, shard_count))
+
+
+def balance_tiles(W: int, H: int, shard_count: int, seg_count: np.ndarray) -> np.ndarray:
+    """octpt_balance_tiles: a tile order that balances shard_count shards by a previous render's per-pixel
+    segment counts (W * H, image order)."""
+    seg = np.ascontiguousarray(seg_count, np.uint32).reshape(-1)
+    if seg.size != W * H:
+        raise ValueError(f"seg_count holds {seg.size} pixels, not {W} x {H}")
+    T = ((W + 7) // 8) * ((H + 7) // 8)
+    order = np.zeros(T, np.uint32)
+    st = _lib.load().octpt_balance_tiles(W, H, shard_count, seg.ctypes.data_as(C.c_void_p),
+                                         order.ctypes.data_as(C.c_void_p))
+    if st != 0:
+        raise _lib.OctptError(st, "octpt_balance_tiles")
+    return order

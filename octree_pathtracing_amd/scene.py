@@ -489,14 +489,27 @@ def procedural_atlas(seed: int, tiles: int = 16, tile: int = 16) -> np.ndarray:
     return out
 
 
+C4_TEXTURES = Path(__file__).resolve().parent / "assets" / "c4_textures.npz"
+
+
+def c4_textures() -> tuple:
+    """(earthmap, greasy): the reference's test_assets/earthmap.jpg (1024x512) and greasy.jpg (3024x4032, box-
+    averaged by 8 to 378x504) as RGBA8 with alpha 255, as RTWImage widens 3-channel images (rtw_image.rs:79-84);
+    decoded once by tools/make_c4_assets.py, the fixture ships in the package (no JPEG decode on the GPU path)."""
+    with np.load(C4_TEXTURES) as z:
+        return z["earthmap"], z["greasy"]
+
+
 def textured_materials(scene: Scene, seed: int) -> dict:
-    """primitive_materials with the diffuse set replaced by image-textured materials (C4: a
-    1024x512 colour map and a 256x256 block atlas)."""
+    """primitive_materials with the diffuse set replaced by image-textured materials (C4, SURVEY.md §8d: the
+    reference's own earthmap and a downsampled greasy, c4_textures; round 4 and before used the procedural
+    stand-ins procedural_terrain / procedural_atlas)."""
     ids = primitive_materials(scene)
-    scene.textures.append(Texture.image(procedural_terrain(seed)))
+    earth, greasy = c4_textures()
+    scene.textures.append(Texture.image(earth))
     scene.materials.append(Material(texture_index=len(scene.textures) - 1))
     terrain = len(scene.materials) - 1
-    scene.textures.append(Texture.image(procedural_atlas(seed)))
+    scene.textures.append(Texture.image(greasy))
     scene.materials.append(Material(texture_index=len(scene.textures) - 1))
     atlas = len(scene.materials) - 1
     ids["diffuse"] = [terrain, atlas]

@@ -7,7 +7,8 @@ FETCH_SIZE reports 1/2 of the bytes of wide reads, so it is doubled.
 The FETCH_SIZE factor defaults to that halving (2); FACTOR overrides it with a calibrated value
 (tools/fetch_calib.hip, profiles/fetch_calib.json) and NOTE says where it came from.
 With TCC_DIR (a --pmc TCC_HIT_sum TCC_MISS_sum pass) the L2 hit rate per kernel is recorded too.
-Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON [FACTOR NOTE [TCC_DIR]]"""
+SOURCE (default: the one-step bench) names the profiled command.
+Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON [FACTOR NOTE [TCC_DIR [SOURCE]]]"""
 import collections
 import csv
 import glob
@@ -36,10 +37,11 @@ def main():
     fetch_dir, write_dir, config, out = sys.argv[1:5]
     factor = float(sys.argv[5]) if len(sys.argv) > 5 else 2.0
     note = sys.argv[6] if len(sys.argv) > 6 else "gfx950 FETCH_SIZE halving of 16-B streaming reads"
-    tcc_dir = sys.argv[7] if len(sys.argv) > 7 else None
+    tcc_dir = sys.argv[7] if len(sys.argv) > 7 and sys.argv[7] else None
+    source = sys.argv[8] if len(sys.argv) > 8 else "python3 bench.py --steps 1"
     ft, fn = per_kernel(fetch_dir, "FETCH_SIZE")
     wt, wn = per_kernel(write_dir, "WRITE_SIZE")
-    res = {"config": config, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, python3 bench.py --steps 1",
+    res = {"config": config, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, {source}",
            "fetch_factor": factor,
            "correction": f"bytes = {factor} * FETCH_SIZE[KiB] * 1024 + WRITE_SIZE[KiB] * 1024 ({note})",
            "raw": {}}

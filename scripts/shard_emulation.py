@@ -2,9 +2,13 @@
 """Strong-scaling rehearsal on one GPU: time every shard of an N-way tile split of the bench
 frame (C3, 1920x1080x256 by default) one after the other.  max over shards ~ the N-GPU step
 time without the RCCL gather; sum/ max = the load-balance ceiling of the speed-up.
-Usage: python scripts/shard_emulation.py [--config C3] [--spp 256] [--ns 1 2 4 8]"""
+--balance: each N-way split under the tile order octpt_balance_tiles derives from the one-GPU frame's per-pixel
+segment counts, instead of the round-robin deal.
+Usage: python scripts/shard_emulation.py [--config C3] [--spp 256] [--ns 1 2 4 8] [--balance]"""
 import argparse
 import json
+
+import numpy as np
 import sys
 import time
 from pathlib import Path
@@ -18,10 +22,11 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--balance", action="store_true")
     args = ap.parse_args()
     import torch
     from octree_pathtracing_amd import scene as S
-    from octree_pathtracing_amd.renderer import HipRenderer, shard_pixels
+    from octree_pathtracing_amd.renderer import HipRenderer, balance_tiles, shard_pixels
 
     sc, cam, rs = S.make_config(args.config)
     if args.spp:
@@ -31,9 +36,18 @@ def main():
     r.set_scene(sc)
     r.set_camera(cam)
     r.max_depth, r.seed = rs.max_depth, rs.seed
-    out = {"config": args.config, "spp": rs.spp, "runs": {}}
+    out = {"config": args.config, "spp": rs.spp, "deal": "balanced" if args.balance else "round robin", "runs": {}}
     stream = torch.cuda.current_stream().cuda_stream
+    seg_full = None
+    if args.balance:  # the one-GPU frame's per-pixel segment counts, the cost the balanced deal evens out
+        acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        seg = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        r.render_device(r.params(W, H, 0, rs.spp), acc.data_ptr(), seg.data_ptr(), stream)
+        torch.cuda.synchronize()
+        seg_full = seg.cpu().numpy().view(np.uint32)
+        del acc, seg
     for n in args.ns:
+        r.set_tile_order(W, H, balance_tiles(W, H, n, seg_full) if args.balance else None)
         times, segs = [], []
         for k in range(n):
             acc = torch.zeros((shard_pixels(W, H, k, n), 4), dtype=torch.float32, device="cuda")

@@ -1,8 +1,10 @@
 """The round-3 stale-hit defect: block_leaf_test with its hit fields written after the alpha
 test's divergent branch (build_variants/prefix: the pre-fix order on today's sources; prefix_check: the same
 with -DOCTPT_CHECK_HITS) against the product library, on the alpha-face world of tests/test_gpu_blocks.py.
+Round 5: variant slotleak_check (-DOCTPT_SLOT_LEAK_PROBE -DOCTPT_CHECK_HITS: advancing lanes take the node slot
+they never loaded) is the negative control of the check build's slot poisoning (SLOT_CHECK).
 Prints one JSON line: per-variant pixels differing from the product render (3 renders each) and the check
-build's hit_check_failures."""
+build's hit_check_failures.  Usage: stale_hit_probe.py [VARIANT ...] (default: prefix prefix_check)"""
 import json
 import sys
 from pathlib import Path
@@ -25,7 +27,7 @@ def main():
     prod = HipRenderer(device=0)
     ref = gpu_render(torch, prod, sc, cam, rs)
     prod.close()
-    for name in ("prefix", "prefix_check"):
+    for name in sys.argv[1:] or ("prefix", "prefix_check"):
         lib = ROOT / "build_variants" / name / "liboctpt.so"
         r = HipRenderer(device=0, lib_path=str(lib))
         runs = []

@@ -30,7 +30,7 @@ RENDERS = {
     "tiny": ("tiny", 64, 48, 4, None),
     "c2_small": ("C2", 160, 90, 4, None),
     "c3_small": ("C3", 96, 54, 2, None),
-    "c4_small": ("C4", 64, 36, 2, None),  # cuboids + image textures (procedural, scene.py)
+    "c4_small": ("C4", 64, 36, 2, None),  # cuboids + image textures (the reference's earthmap / greasy, scene.c4_textures)
     "c5_small": ("C5", 96, 54, 2, None),  # 1 M unit-block voxel terrain + block models, depth 11
     "blocks_small": ("blocks", 64, 48, 4, None),  # block-model quads
     # sun sampling (next-event estimation): config + scene.SUN_VARIANTS entry
@@ -45,7 +45,7 @@ RENDERS = {
 # RendererMode::Preview fixtures: name -> (config, width, height)
 PREVIEWS = {
     "c3_preview": ("C3", 192, 108),
-    "c4_preview": ("C4", 128, 72),  # transparent texels exercise the pass-through loop
+    "c4_preview": ("C4", 128, 72),  # the glass material's alpha-0 texels exercise the pass-through loop
     "c5_preview": ("C5", 160, 90),
     "blocks_preview": ("blocks", 128, 96),
 }

@@ -152,9 +152,11 @@ def assert_parity_shipped(gpu, ref, tag):
     racc, rsegs, rst = ref
     assert np.array_equal(segs, rsegs), f"{tag}: per-pixel segment counts differ at {np.argwhere(segs != rsegs)[:5]}"
     assert st["segments"] == rst["segments"], tag
-    assert st["esvo_steps"] <= rst["esvo_steps"], (tag, st["esvo_steps"], rst["esvo_steps"])
     # a camera ray whose beam start reached the step cap is traced again from the cube entry (beam_restarts):
-    # the leaf tests of its first walk are work done on top of the reference's
+    # its first walk's iterations (at most the 1000-iteration cap) and leaf tests are work done on top of the
+    # reference's (the stated relaxation of the totals; radiance and segments stay exact)
+    cap = 1000 * st["beam_restarts"]
+    assert st["esvo_steps"] <= rst["esvo_steps"] + cap, (tag, st["esvo_steps"], rst["esvo_steps"], cap)
     tests, ref_tests = st["sphere_tests"] + st["cuboid_tests"], rst["prim_tests"]
     blocks, ref_blocks = st.get("block_tests", 0), rst.get("block_tests", 0)
     if st["beam_restarts"] == 0:
@@ -185,6 +187,25 @@ def test_beam_fullframe_oracle(torch_cuda, beam, name, spp):
     exact = assert_parity_shipped(gpu, ref, name)
     assert exact > 0.999, f"{name}: only {exact:.4%} of channels bit-identical"
     assert gpu[2]["esvo_steps"] < ref[2]["esvo_steps"], name  # the beam did skip iterations
+
+
+def test_c2_fullframe_oracle(torch_cuda, renderer, beam):
+    """C2 at its full BASELINE size (1280x720, 100 spheres, depth 6) with 8 of its 64 spp (VERDICT r04 item 5;
+    the render loop of tile_renderer.rs:684-734): the shipped default (beam on) against the oracle, and the
+    beam-off render exactly, iteration total included."""
+    from octree_pathtracing_amd import scene as S
+    from tests.test_gpu_parity import assert_parity, oracle
+
+    sc, cam, rs = S.make_config("C2")
+    assert (rs.width, rs.height) == (1280, 720)
+    rs.spp = 8
+    ref = oracle(sc, cam, rs, forward=True, threads=16)
+    on = gpu_render(torch_cuda, beam, sc, cam, rs)
+    assert on[2]["paths"] == 1280 * 720 * 8
+    exact = assert_parity_shipped(on, ref, "C2 beam")
+    assert exact > 0.999 and on[2]["esvo_steps"] < ref[2]["esvo_steps"]
+    off = gpu_render(torch_cuda, renderer, sc, cam, rs)
+    assert_parity(off, ref, "C2 no beam")
 
 
 @pytest.mark.parametrize("name", ["C3", "C5b"])

@@ -26,13 +26,25 @@ def _bench(tmp_path, n, extra=()):
 
 def test_two_ranks_gather_equals_one(tmp_path):
     one, f1 = _bench(tmp_path, 1)
-    two, f2 = _bench(tmp_path, 2, ("--dist-backend", "gloo"))
+    # one warmup step: its per-tile segment counts give the balanced tile deal of the timed step
+    two, f2 = _bench(tmp_path, 2, ("--dist-backend", "gloo", "--warmup", "1"))
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
-    assert two["config"]["parallelism"] == "tiles2-gloo"
+    assert two["config"]["parallelism"] == "tiles2-gloo" and two["config"]["tile_deal"].startswith("balanced")
     assert f1.shape == f2.shape == (1280 * 720, 4)
     assert np.array_equal(f1, f2)
     # every rank's segments are counted once
     assert one["config"]["segments_per_step"] == two["config"]["segments_per_step"]
+    # the N-rank roofline: per-rank figures, the aggregate is their sum over the slowest
+    # rank's extend time, achieved their mean, and no one-GPU PMC traffic on a two-rank line
+    rf = two["roofline"]
+    ranks = rf["ranks"]
+    assert [x["rank"] for x in ranks] == [0, 1] and all(x["bytes"] > 0 and x["ext_ms"] > 0 for x in ranks)
+    tmax = max(x["ext_ms"] for x in ranks) / 1e3
+    assert rf["aggregate_gbs"] == pytest.approx(sum(x["bytes"] for x in ranks) / tmax / 1e9, rel=1e-3)
+    assert rf["achieved"] == pytest.approx(sum(x["achieved"] for x in ranks) / 2, rel=1e-3)
+    assert rf["aggregate_peak"] == 2 * rf["peak"] and rf["frac_min"] <= rf["frac"] <= rf["frac_max"]
+    assert rf["traffic"] is None and "pmc_C2_n2.json" in rf["traffic_source"]
+    assert one["roofline"]["achieved"] > 0 and "ranks" not in one["roofline"]
     # rank 0's measurement of the same frame through one multi-device context (octpt_create_multi):
     # on this box its two entries repeat device 0
     cm = two["capi_multi"]

@@ -177,6 +177,38 @@ def test_intersect_parity(renderer):
         assert np.array_equal(t[hit], rt[hit]) and np.array_equal(nrm, rnrm), name
 
 
+def test_intersect_unsupported_rays_are_misses(renderer):
+    """A ray with a non-finite component or a direction component above 2^126 is a miss (the
+    reference's Scene::hit takes any ray), and the batch's other rays are traced exactly as without it."""
+    from octree_pathtracing_amd import scene as S
+    from oracle import cpu_ref
+
+    sc, _, _ = S.make_config("C3")
+    renderer.set_scene(sc)
+    rng = np.random.default_rng(11)
+    n = 4096
+    world = float(2 ** sc.octree.depth)
+    o = rng.uniform(0.1 * world, 0.9 * world, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    want = cpu_ref.intersect(sc, rays)
+    bad = rays.copy()
+    bad_rows = [3, 100, 101, 2000, n - 1]
+    bad[3, 0] = np.nan
+    bad[100, 4] = np.inf
+    bad[101, 5] = -np.inf
+    bad[2000, 3] = 2.0 ** 127
+    bad[n - 1, 1] = -np.inf
+    t, prim, nrm, steps = renderer.intersect(bad)
+    keep = np.setdiff1d(np.arange(n), bad_rows)
+    assert np.all(np.isposinf(t[bad_rows])) and np.all(prim[bad_rows] == 0xFFFFFFFF)
+    assert np.all(nrm[bad_rows] == 0) and np.all(steps[bad_rows] == 0)
+    assert np.array_equal(prim[keep], want[1][keep]) and np.array_equal(steps[keep], want[3][keep])
+    hit = keep[want[1][keep] != 0xFFFFFFFF]
+    assert len(hit) > 100 and np.array_equal(t[hit], want[0][hit]) and np.array_equal(nrm[keep], want[2][keep])
+
+
 def test_tonemap_parity(torch_cuda, renderer):
     from oracle import cpu_ref
 

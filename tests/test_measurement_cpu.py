@@ -101,6 +101,29 @@ def test_bench_loads_committed_traffic():
     traffic, src, l2 = bench.load_traffic("C3")
     assert traffic and traffic > 0 and "pmc_C3.json" in src
     assert l2 is None or 0.0 < l2 < 1.0
-    assert bench.load_traffic("no-such-config") == (None, None, None)
+    t, why, l2 = bench.load_traffic("no-such-config")
+    assert t is None and l2 is None and "no PMC profile" in why
+    # a line at N ranks never quotes the one-GPU profile
+    t8, why8, _ = bench.load_traffic("C3", 8)
+    if not (ROOT / "profiles" / "pmc_C3_n8.json").exists():
+        assert t8 is None and "pmc_C3_n8.json" in why8
+    else:
+        assert t8 != traffic and "pmc_C3_n8.json" in why8
     h = bench.host_cpu()
     assert h["threads"] >= 1 and h["affinity"] >= 1 and h["model"]
+
+
+def test_roofline_over_ranks():
+    """The N-rank line's extend roofline: per-GPU mean, aggregate over the slowest rank's
+    time, per-rank spread; one rank reduces to bytes / time."""
+    import bench
+
+    one = bench.roofline_over_ranks([{"bytes": 8e12, "ext_ms": 2000.0, "launches": 9}])
+    assert one["achieved"] == 4000.0 and one["frac"] == 0.5 and one["aggregate_gbs"] == 4000.0
+    assert one["aggregate_peak"] == 8000.0 and one["frac_min"] == one["frac_max"] == 0.5
+    r = bench.roofline_over_ranks([{"bytes": 4e12, "ext_ms": 1000.0, "launches": 9},
+                                   {"bytes": 3e12, "ext_ms": 1500.0, "launches": 9}])
+    assert r["achieved"] == (4000.0 + 2000.0) / 2 and r["frac"] == 0.375
+    assert r["aggregate_gbs"] == round(7e12 / 1.5 / 1e9, 1) and r["aggregate_peak"] == 16000.0
+    assert r["frac_min"] == 0.25 and r["frac_max"] == 0.5
+    assert sum(x["bytes"] for x in r["per_rank"]) == 7e12 and [x["rank"] for x in r["per_rank"]] == [0, 1]
