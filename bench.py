@@ -319,9 +319,10 @@ def main():
     ap.add_argument("--capi-devices", default=None,
                     help="one process, one multi-device context (octpt_create_multi) over N devices or a list of "
                          "HIP ids: the C-ABI path a Rust host calls (DESIGN.md §9); ids repeat on a one-GPU box")
-    ap.add_argument("--no-balance", action="store_true",
-                    help="with N > 1 ranks, keep the round-robin tile deal instead of the order octpt_balance_tiles "
-                         "derives from the warmup step's per-tile segment counts (DESIGN.md §9)")
+    ap.add_argument("--balance", action="store_true",
+                    help="with N > 1 ranks, time the steps under the tile order octpt_balance_tiles derives from the "
+                         "warmup step's per-tile segment counts instead of the round-robin deal (DESIGN.md §9: "
+                         "measured equal on C3 / C5b, so round robin stays the default)")
     ap.add_argument("--no-capi-multi", action="store_true",
                     help="with N > 1 ranks, skip rank 0's extra measurement of the same frame through one "
                          "multi-device context over the N devices")
@@ -393,7 +394,7 @@ def main():
             g = gbuf_dev
         r.unshard_device(W, H, world, g.data_ptr(), stride, frame.data_ptr(), stream)
 
-    balance = world > 1 and not args.no_balance and args.warmup > 0
+    balance = world > 1 and args.balance and args.warmup > 0
     segbuf = torch.zeros(stride, dtype=torch.int32, device=dev) if balance else None
 
     def step(seg=None):

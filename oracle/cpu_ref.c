@@ -737,18 +737,20 @@ static int block_leaf_test(ctx_t *c, const ray_t *r, uint32_t block, v3 pos, flo
 #ifdef REF_ESVO_TRACE
 /* diagnostic build only (tools/esvo_trace.py): one byte per ESVO iteration, single-threaded renders.
  * low 3 bits: 0 advance over an absent child, 1 leaf test missed, 2 leaf hit, 3 descend, 4 advance
- * past a present child not entered; 8 = the advance popped; 16 = first iteration of a ray */
+ * past a present child not entered; 8 = the advance popped; 16 = first iteration of a ray; 32 = the ray
+ * leaves a primitive (a bounce / continue ray, last_prim set) */
 static uint8_t *g_trace;
 static size_t g_trace_n, g_trace_cap;
-static int g_trace_first;
+static int g_trace_first, g_trace_bounce;
 static void trace_put(int code) {
-    if (g_trace_n < g_trace_cap) g_trace[g_trace_n++] = (uint8_t)(code | (g_trace_first ? 16 : 0));
+    if (g_trace_n < g_trace_cap)
+        g_trace[g_trace_n++] = (uint8_t)(code | (g_trace_first ? 16 : 0) | (g_trace_bounce ? 32 : 0));
     g_trace_first = 0;
 }
 void ref_esvo_trace_set(uint8_t *buf, size_t cap) { g_trace = buf; g_trace_cap = cap; g_trace_n = 0; }
 size_t ref_esvo_trace_len(void) { return g_trace_n; }
 #define TRACE(c) trace_put(c)
-#define TRACE_BEGIN() (g_trace_first = 1)
+#define TRACE_BEGIN() (g_trace_first = 1, g_trace_bounce = ray->last_prim != PRIM_NONE)
 #else
 #define TRACE(c) ((void)0)
 #define TRACE_BEGIN() ((void)0)

@@ -27,7 +27,7 @@ def _bench(tmp_path, n, extra=()):
 def test_two_ranks_gather_equals_one(tmp_path):
     one, f1 = _bench(tmp_path, 1)
     # one warmup step: its per-tile segment counts give the balanced tile deal of the timed step
-    two, f2 = _bench(tmp_path, 2, ("--dist-backend", "gloo", "--warmup", "1"))
+    two, f2 = _bench(tmp_path, 2, ("--dist-backend", "gloo", "--warmup", "1", "--balance"))
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["config"]["parallelism"] == "tiles2-gloo" and two["config"]["tile_deal"].startswith("balanced")
     assert f1.shape == f2.shape == (1280 * 720, 4)

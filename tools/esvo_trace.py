@@ -43,10 +43,23 @@ def main():
     kind = t & 7
     pop = (t & 8) != 0
     first = (t & 16) != 0
+    bounce = (t & 32) != 0
     print(f"{cfg} {W}x{H}x{spp}: {st['segments']} segments, {n} iterations ({n / st['segments']:.1f}/segment)")
     names = {0: "absent-advance", 1: "leaf miss", 2: "leaf hit", 3: "descend", 4: "present, not entered"}
     for k, v in sorted(Counter(kind.tolist()).items()):
         print(f"  {names[k]:22s} {v / n:6.1%}   popped {np.mean(pop[kind == k]):.1%}")
+    # the leading descends of each ray (iterations before its first non-descend): what a start at the
+    # ray's origin cell would skip (bounce rays from their leaf)
+    ray_id = np.cumsum(first) - 1
+    nd = kind != 3
+    first_nd = np.full(ray_id[-1] + 1, n, np.int64)
+    np.minimum.at(first_nd, ray_id[nd], np.nonzero(nd)[0])
+    starts = np.nonzero(first)[0]
+    lead = np.minimum(first_nd, np.append(starts[1:], n)) - starts
+    rb = bounce[starts]
+    print(f"  leading descends: bounce rays {lead[rb].mean():.2f} per ray ({rb.mean():.1%} of rays), camera rays "
+          f"{lead[~rb].mean():.2f}; bounce rays' leading descends = {lead[rb].sum() / n:.1%} of all iterations, "
+          f"{lead[rb].sum() / max(int((bounce).sum()), 1):.1%} of bounce rays' iterations")
     # folding: an absent-advance folds into the previous iteration of the same ray when that
     # iteration did not pop (K: at most K folds per iteration); optionally after a pop too
     seq = kind.tolist()
