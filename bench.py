@@ -71,12 +71,20 @@ def lean_state(sc, st: dict) -> bool:
             and os.environ.get("OCTPT_LEAN", "") != "0")
 
 
-def shade_bytes(st: dict, lean: bool = False) -> float:
-    """DESIGN.md §8, wf_shade_kernel per segment: ray record 32 + hit 8 + path state read, path state +
-    ray record 32 written (the path state 40 B, or 24 B in the lean state); per shaded hit 16 (sphere) +
-    4 (material id) + 48 (material record); 4 B per texel; 16 B per finished path (colour record)."""
+def shade_bytes(st: dict, lean: bool = False, lds_tables: bool = False) -> float:
+    """DESIGN.md §8, wf_shade_kernel's global-memory bytes per segment: ray record 32 + hit 8 + path state read, path
+    state + ray record 32 written (the path state 40 B, or 24 B in the lean state); per shaded hit 16 (sphere or box
+    record) + 4 (material id) + 48 (material record, unless the scene's material tables sit in LDS: lds_tables,
+    shade_lds_tables); 4 B per texel; 16 B per finished path (colour record).  Until round 4 the 48 B of an
+    LDS-resident material record were counted too."""
     per_seg = 40.0 + 2.0 * (24.0 if lean else 40.0) + 32.0
-    return (per_seg * st["segments"] + 68.0 * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
+    per_event = 20.0 + (0.0 if lds_tables else 48.0)
+    return (per_seg * st["segments"] + per_event * st["shade_events"] + 4.0 * st["texel_reads"] + 16.0 * st["paths"])
+
+
+def shade_lds_tables(sc) -> bool:
+    """Whether shade reads the material / texture tables from LDS (octpt_kernels.hip shade_lds_tables: <= 128 of each)."""
+    return len(sc.materials) <= 128 and len(sc.textures) <= 128
 
 
 def pmc_name(config: str, world: int = 1) -> str:
@@ -438,7 +446,7 @@ def main():
     n_sh = max(st["shade_launches"], 1)
     sh_s = st["shade_ms"] / 1e3 / n_sh
     lean = lean_state(sc, st)
-    sh_bytes = shade_bytes(st, lean) / n_sh
+    sh_bytes = shade_bytes(st, lean, shade_lds_tables(sc)) / n_sh
     traffic, traffic_src, l2_hit = load_traffic(args.config, world)
     out = {
         "metric": METRIC,
@@ -487,7 +495,10 @@ def main():
             "shade": {"kernel": "wf_shade_kernel", "launches": st["shade_launches"],
                       "kernel_ms_avg": round(sh_s * 1e3, 4), "algorithmic_bytes_per_launch": int(sh_bytes),
                       "achieved": round(sh_bytes / sh_s / 1e9, 1) if sh_s > 0 else 0.0,
-                      "path_state_bytes": 24 if lean else 40},
+                      "path_state_bytes": 24 if lean else 40,
+                      "bytes_basis": "global-memory bytes of the shade model (DESIGN.md §8): queue + path state + "
+                                     "primitive records + texels + colour records; LDS-resident material tables "
+                                     "excluded; latency-bound, not at its bandwidth"},
         },
         "stats_rank0": {k: v for k, v in st.items() if k != "kernel_ms"},
     }

@@ -2604,7 +2604,7 @@ __device__ __forceinline__ float beam_pack(float t, uint32_t nodes) {
 // Round 5: kBeamLanes lanes per beam tile, lane j standing for child j of the octant the
 // walk is in.  Entering an octant tests its eight children's boxes at once (while its node slot is in flight),
 // and each iteration takes the nearest child still nearer than the best leaf so far (a min over the group's
-// eight lanes, three xor shuffles), so the walk's sequential length is the number of cells it takes, not the
+// eight lanes, three DPP moves), so the walk's sequential length is the number of cells it takes, not the
 // number of children it tests; eight tiles share a 64-lane wave, and an 8-way shard's 16 K C3 tiles fill
 // 2 K waves instead of 253.  The start is the same distance (the minimum over the pyramid's leaf cells, by the
 // same box arithmetic), so only the walk's octant count -- the iteration bound it packs -- differs.
@@ -2658,58 +2658,74 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
     };
     const float lod = kBeamLod * fmaxf(s1 - s0, t1 - t0) / sqrtf(vdot(F, F));
     float best = __builtin_inff();
-    // LDS, for the scene's depth levels (launch_beam sizes it: (64 + 5 x 8) x depth x 4 B, 3.3 KB at depth 8):
-    // st_d[level][thread] = the distance of child `lane` of the level's octant (+inf: absent, outside the
-    // pyramid, or taken), and per group the octant's slot base, mask and low corner (every lane of the group
-    // writes the same value: no lane-0 branch)
+    // The walk's current octant lives in registers -- its slot base, mask and low corner, and dj, this lane's
+    // child distance (+inf: absent, outside the pyramid, or taken) -- and its ancestors in LDS, saved when the walk
+    // descends and reloaded when it pops (launch_beam sizes it: (64 + 5 x 8) x depth x 4 B, 3.3 KB at depth 8):
+    // st_d[level][thread], and per group the slot base, mask and corner (every lane of a group writes the same
+    // value: no lane-0 branch).  Taking a leaf touches no memory at all.
     extern __shared__ uint32_t beam_lds[];
     const uint32_t t = threadIdx.x, L = beam_levels(S.depth);
     constexpr uint32_t G = 64u / kBeamLanes;
     float *const st_d = reinterpret_cast<float *>(beam_lds);
     uint32_t *const st_base = beam_lds + L * 64u, *const st_mask = st_base + L * G;
     float *const st_lx = reinterpret_cast<float *>(st_mask + L * G), *const st_ly = st_lx + L * G, *const st_lz = st_ly + L * G;
-    // child `lane` of the octant at `lo` (children of size hc) with mask m: its distance, or +inf
-    auto child_d = [&](v3 lo, float hc, uint32_t m) -> float {
-        const v3 clo = V(lo.x + ((lane & 1u) ? hc : 0.0f), lo.y + ((lane & 2u) ? hc : 0.0f), lo.z + ((lane & 4u) ? hc : 0.0f));
-        const float d = box(clo, hc);
-        return (((m >> lane) & 1u) != 0u && d >= 0.0f) ? d : __builtin_inff();
+    // the minimum of a lane value over the group's 8 lanes in three DPP moves: xor 1 and xor 2 inside each quad
+    // (quad_perm 1,0,3,2 and 2,3,0,1), then the half-row mirror (lane i <- 7 - i) between the two quads
+    auto grp_min = [](uint32_t k) {
+        k = min(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0xB1, 0xF, 0xF, false));
+        k = min(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x4E, 0xF, 0xF, false));
+        k = min(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x141, 0xF, 0xF, false));
+        return k;
     };
+    // the box distance of child `lane` of the octant at `lo` (children of size hc), or -1 outside the pyramid
+    auto child_box = [&](v3 lo, float hc) -> float {
+        return box(V(lo.x + ((lane & 1u) ? hc : 0.0f), lo.y + ((lane & 2u) ? hc : 0.0f), lo.z + ((lane & 4u) ? hc : 0.0f)),
+                   hc);
+    };
+    auto present_d = [&](float db, uint32_t m) { return (((m >> lane) & 1u) != 0u && db >= 0.0f) ? db : __builtin_inff(); };
     bool exhausted = S.depth >= (uint32_t)kBeamLevels;
     uint32_t nodes = 1u;  // octants the walk entered (the root included)
     if (!exhausted && box(V(1.0f, 1.0f, 1.0f), 1.0f) >= 0.0f) {
         int lv = 0;
-        st_base[grp] = S.root;
-        st_mask[grp] = S.root_mask;
-        st_lx[grp] = st_ly[grp] = st_lz[grp] = 1.0f;
-        st_d[t] = child_d(V(1.0f, 1.0f, 1.0f), 0.5f, S.root_mask);
+        uint32_t cbase = S.root, cmask = S.root_mask;
+        v3 clo = V(1.0f, 1.0f, 1.0f);
+        float dj = present_d(child_box(clo, 0.5f), cmask);
         uint32_t visits = 0u;
-        while (lv >= 0) {  // group-uniform control flow: every decision below is the group's
-            const float dj = st_d[lv * 64 + t];
-            // the nearest child still nearer than best: its distance's bits (>= 0, so ordered as unsigned)
-            // with the lane in the low 3 bits, minimised over the group
-            uint32_t k = dj < best ? ((__float_as_uint(dj) & ~7u) | lane) : 0xFFFFFFFFu;
-            k = min(k, (uint32_t)__shfl_xor((int)k, 1, kBeamLanes));
-            k = min(k, (uint32_t)__shfl_xor((int)k, 2, kBeamLanes));
-            k = min(k, (uint32_t)__shfl_xor((int)k, 4, kBeamLanes));
-            if (k == 0xFFFFFFFFu) { --lv; continue; }
+        for (;;) {  // group-uniform control flow: every decision below is the group's
+            // the nearest child still nearer than best: its distance's bits (>= 0, so ordered as unsigned) with the
+            // lane in the low 3 bits, minimised over the group
+            const uint32_t k = grp_min(dj < best ? ((__float_as_uint(dj) & ~7u) | lane) : 0xFFFFFFFFu);
+            if (k == 0xFFFFFFFFu) {  // this octant is done: back to its parent
+                if (--lv < 0) break;
+                dj = st_d[lv * 64 + t];
+                cbase = st_base[lv * G + grp];
+                cmask = st_mask[lv * G + grp];
+                clo = V(st_lx[lv * G + grp], st_ly[lv * G + grp], st_lz[lv * G + grp]);
+                continue;
+            }
             if (++visits > kBeamVisits) { exhausted = true; break; }
             const uint32_t ci = k & 7u;
-            const float d = __shfl(dj, (int)ci, kBeamLanes);  // its exact distance
-            if (lane == ci) st_d[lv * 64 + t] = __builtin_inff();
-            const uint32_t m = st_mask[lv * G + grp], kind = (m >> ci) & 0x101u;
+            // its distance with the low 3 bits cleared: at most 7 ulp below it, so best, and the start, can only
+            // come out nearer (conservative), and every octant nearer than the final start is still entered
+            const float d = __uint_as_float(k & ~7u);
+            if (lane == ci) dj = __builtin_inff();
+            const uint32_t kind = (cmask >> ci) & 0x101u;
             const float h = __uint_as_float((126u - (uint32_t)lv) << 23);  // 2^-(lv + 1)
             if (kind == 0x101u || lv + 1 >= (int)L || h <= lod * d) { best = d; continue; }  // leaf / small cell
-            const uint2 slot = S.node_child[st_base[lv * G + grp] + __popc(m & ((1u << ci) - 1u))];
-            const v3 lo = V(st_lx[lv * G + grp] + ((ci & 1u) ? h : 0.0f), st_ly[lv * G + grp] + ((ci & 2u) ? h : 0.0f),
-                            st_lz[lv * G + grp] + ((ci & 4u) ? h : 0.0f));
+            const uint2 slot = S.node_child[cbase + __popc(cmask & ((1u << ci) - 1u))];
+            st_d[lv * 64 + t] = dj;  // this octant's remaining children, for the pop back to it
+            st_base[lv * G + grp] = cbase;
+            st_mask[lv * G + grp] = cmask;
+            st_lx[lv * G + grp] = clo.x;
+            st_ly[lv * G + grp] = clo.y;
+            st_lz[lv * G + grp] = clo.z;
+            clo = V(clo.x + ((ci & 1u) ? h : 0.0f), clo.y + ((ci & 2u) ? h : 0.0f), clo.z + ((ci & 4u) ? h : 0.0f));
+            const float db = child_box(clo, h * 0.5f);  // while the slot is in flight
             ++lv;
             ++nodes;
-            st_base[lv * G + grp] = slot.x;
-            st_mask[lv * G + grp] = slot.y;
-            st_lx[lv * G + grp] = lo.x;
-            st_ly[lv * G + grp] = lo.y;
-            st_lz[lv * G + grp] = lo.z;
-            st_d[lv * 64 + t] = child_d(lo, h * 0.5f, slot.y);
+            cbase = slot.x;
+            cmask = slot.y;
+            dj = present_d(db, cmask);
         }
     }
     if (lane == 0u) beam[tile] = exhausted ? 0.0f : beam_pack(best * (1.0f - 0x1p-16f), nodes);
