@@ -151,3 +151,50 @@ def test_order_validation(torch_cuda, renderer):
         gpu_render(torch_cuda, r, sc, cam, rs2)
     finally:
         r.close()
+
+
+def test_order_regeneration_branches_async(torch_cuda, renderer):
+    """A tile order under the other paths that map items to pixels: a pool smaller than the chunk (shade
+    regenerates camera rays, beam on), a branch schedule (C20), and the asynchronous frame (octpt_render_async)."""
+    import os
+
+    from octree_pathtracing_amd import scene as S
+    from octree_pathtracing_amd.renderer import HipRenderer
+
+    sc, cam, rs = S.make_config("tiny")
+    rs.width, rs.height, rs.spp = 70, 45, 8
+    W, H = rs.width, rs.height
+    order = _shuffled(W, H, 21)
+    old = {k: os.environ.get(k) for k in ("OCTPT_BEAM", "OCTPT_POOL", "OCTPT_CHUNK")}
+    os.environ.update(OCTPT_BEAM="1", OCTPT_POOL="4096", OCTPT_CHUNK="8192")
+    try:
+        small = HipRenderer(device=0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        for bc in (1, 4):
+            ref = gpu_render(torch_cuda, small, sc, cam, rs, branch_count=bc)
+            small.set_tile_order(W, H, order)
+            got = gpu_render(torch_cuda, small, sc, cam, rs, branch_count=bc)
+            small.set_tile_order(W, H, None)
+            assert np.array_equal(got[0].view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(got[1], ref[1]), bc
+            for k in SAME:
+                assert got[2][k] == ref[2][k], (bc, k)
+        small.set_scene(sc)
+        small.set_camera(cam)
+        small.set_resolution((W, H))
+        small.max_depth, small.seed = rs.max_depth, rs.seed
+        small.branch_count = 1
+        want = small.render_frame(spp_count=4).wait_for().copy()
+        want_f = np.array(small.get_float_image(), copy=True)
+        small.reset_render()
+        small.set_tile_order(W, H, order)
+        got = small.render_frame(spp_count=4).wait_for()
+        assert np.array_equal(got, want)
+        assert np.array_equal(np.asarray(small.get_float_image()).view(np.uint32), want_f.view(np.uint32))
+    finally:
+        small.close()
