@@ -272,6 +272,7 @@ def capi_multi_measure(sc, cam, rs, devices, steps: int, warmup: int) -> dict:
             r.reset_stats()
             t0 = time.perf_counter()
             for _ in range(steps):
+                r.set_camera(cam)  # the beam tables recomputed every step, as in the main loop
                 r.render_device(p, acc.data_ptr(), None, stream)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
@@ -407,6 +408,9 @@ def main():
 
     def step(seg=None):
         stream = torch.cuda.current_stream().cuda_stream
+        # the camera set again: the beam table is recomputed every step (a render with an unchanged camera would
+        # reuse it, as a progressive renderer's next frame does), so a step carries the whole frame's work
+        r.set_camera(cam)
         r.render_device(params, accum.data_ptr(), seg.data_ptr() if seg is not None else None, stream)
         if world > 1:  # gather to rank 0 (RCCL over xGMI), then the unshard kernel on rank 0
             src = accum.cpu() if host_staged else accum

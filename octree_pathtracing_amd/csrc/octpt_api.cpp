@@ -139,6 +139,19 @@ struct octpt_ctx {
     std::vector<uint32_t> h_order;
     uint32_t order_w = 0, order_h = 0;
     uint32_t *d_order = nullptr, *d_order_pos = nullptr;
+    // what the beam table in d_beam was computed for (round 5): the scene, camera and tile order (their
+    // generations) and the frame size and shard.  A render with the same key reuses it -- a progressive
+    // renderer calls render_frame again and again with one camera -- and anything else recomputes it.
+    uint64_t scene_gen = 0, camera_gen = 0, order_gen = 0;
+    struct BeamKey {
+        uint64_t scene = 0, camera = 0, order = 0;
+        uint32_t w = 0, h = 0, shard_index = 0, shard_count = 0;
+        bool valid = false;
+        bool operator==(const BeamKey &o) const {
+            return valid && o.valid && scene == o.scene && camera == o.camera && order == o.order && w == o.w &&
+                   h == o.h && shard_index == o.shard_index && shard_count == o.shard_count;
+        }
+    } beam_key;
 };
 
 struct octpt_frame {
@@ -960,15 +973,29 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
     const float *beam = nullptr;
     if (ctx->beam) {
         const size_t n_tiles = (size_t)R.beam_tx * ((R.H + kBeamTile - 1) / kBeamTile);
+        octpt_ctx::BeamKey key;
+        key.scene = ctx->scene_gen;
+        key.camera = ctx->camera_gen;
+        key.order = ctx->order_gen;
+        key.w = R.W;
+        key.h = R.H;
+        key.shard_index = R.shard_index;
+        key.shard_count = R.shard_count;
+        key.valid = true;
         if (n_tiles > ctx->beam_cap) {
             HIP_TRY(ctx, hipDeviceSynchronize());  // an earlier render may still read the table
             if (ctx->d_beam) (void)hipFree(ctx->d_beam);
             ctx->d_beam = nullptr;
             ctx->beam_cap = 0;
+            ctx->beam_key.valid = false;
             HIP_TRY(ctx, hipMalloc(&ctx->d_beam, n_tiles * sizeof(float)));
             ctx->beam_cap = n_tiles;
         }
-        HIP_TRY(ctx, launch_beam(ctx->S, ctx->C, R, ctx->d_beam, s));
+        if (!(key == ctx->beam_key)) {  // same scene, camera, size, shard and deal: the table is already there
+            ctx->beam_key.valid = false;
+            HIP_TRY(ctx, launch_beam(ctx->S, ctx->C, R, ctx->d_beam, s));
+            ctx->beam_key = key;
+        }
         beam = ctx->d_beam;
     }
     for (uint32_t c0 = 0, c1 = 0; c0 < R.spp_count; c0 = c1) {
@@ -1589,6 +1616,7 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         if (st != OCTPT_OK) return st;
         ctx->S = S;
         ctx->has_scene = true;
+        ++ctx->scene_gen;
         return OCTPT_OK;
     } catch (const std::bad_alloc &) {
         free_scene(ctx);
@@ -1665,6 +1693,7 @@ octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *d,
         if (st != OCTPT_OK) return st;
         ctx->S = S;
         ctx->has_scene = true;
+        ++ctx->scene_gen;
         return OCTPT_OK;
     } catch (const std::bad_alloc &) {
         free_scene(ctx);
@@ -1689,6 +1718,7 @@ octpt_status octpt_set_camera(octpt_ctx *ctx, const octpt_camera *c) {
     C.d_factor = 1.0f / tanf(c->fov / 2.0f);         // camera.rs:79
     ctx->C = C;
     ctx->has_camera = true;
+    ++ctx->camera_gen;
     for (octpt_ctx *sc : ctx->sub) {
         const octpt_status st = octpt_set_camera(sc, c);
         if (st != OCTPT_OK) return fail(ctx, st, sc->err);
@@ -1881,6 +1911,7 @@ octpt_status octpt_set_tile_order(octpt_ctx *ctx, uint32_t width, uint32_t heigh
             if (st != OCTPT_OK) return fail(ctx, st, c->err);
         }
         HIP_TRY(ctx, hipSetDevice(ctx->device));
+        ++ctx->order_gen;
         if (!order) {
             ctx->h_order.clear();
             ctx->order_w = ctx->order_h = 0;

@@ -18,7 +18,7 @@ constexpr uint32_t kPrimCuboidBit = 0x80000000u;
 constexpr uint32_t kPrimIndexMask = 0x07FFFFFFu;  // primitive indices < 2^27 (hit records pack flags above)
 // camera-ray beam starts (beam_kernel): one per kBeamTile x kBeamTile pixels (A/B knob)
 #ifndef OCTPT_BEAM_TILE
-#define OCTPT_BEAM_TILE 4
+#define OCTPT_BEAM_TILE 2
 #endif
 constexpr uint32_t kBeamTile = OCTPT_BEAM_TILE;
 constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primary rays

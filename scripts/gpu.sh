@@ -8,7 +8,8 @@
 #   smoke                 __graft_entry__.smoke()                                  -> smoke.log
 #   bench:CFG[:STEPS]     one bench line of CFG (CPU baseline + issued probe)      -> bench_CFG.json
 #   fast:CFG[:STEPS]      the same without the CPU baseline                         -> bench_CFG.json
-#   stats:CFG             rocprofv3 --kernel-trace --stats of that bench command    -> stats_CFG/
+#   stats:CFG[:STEPS[:LIB]]  rocprofv3 --kernel-trace --stats of that bench command  -> stats_CFG/
+#                         (LIB = build_variants/NAME/liboctpt.so runs that build -> stats_CFG_NAME/)
 #   pmc:CFG[:N]           FETCH_SIZE / WRITE_SIZE / TCC passes: the one-step bench (N = 1) or rank 0's shard of
 #                         an N-way split (scripts/shard_step.py) -> pmc_CFG[_nN].json, also into profiles/
 #   sq:CFG                the SQ counter pass of the one-step bench                 -> sq_CFG/
@@ -41,10 +42,12 @@ for task in "$@"; do
           2> $O/bench_${a:-C3}.err || fail "$task" $O/bench_${a:-C3}.err
       cat $O/bench_${a:-C3}.json ;;
     stats)
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/stats_$a -o run \
+      V=$a; if [ -n "$c" ]; then V=${a}_$(basename $(dirname $c)); fi
+      (cd /tmp && export TMPDIR=/tmp && if [ -n "$c" ]; then export OCTPT_LIB=$R/$c; fi \
+          && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/stats_$V -o run \
           --output-format csv -- python3 $R/bench.py --config $a --steps ${b:-5} --warmup 1 --no-cpu-baseline \
-          > $O/stats_$a.json 2> $O/stats_$a.err) || fail "$task" $O/stats_$a.err
-      cat $O/stats_$a.json ;;
+          > $O/stats_$V.json 2> $O/stats_$V.err) || fail "$task" $O/stats_$V.err
+      cat $O/stats_$V.json ;;
     pmc)
       N=${b:-1}; SUF=""; [ $N -gt 1 ] && SUF=_n$N
       if [ $N -gt 1 ]; then CMD="$R/scripts/shard_step.py --config $a --n $N --k 0"; SRC="python3 scripts/shard_step.py --config $a --n $N --k 0 (rank 0's shard of an $N-way split, one step)"

@@ -44,6 +44,7 @@ def main():
             r.render_device(p, acc.data_ptr(), None, stream)
         torch.cuda.synchronize()
         r.reset_stats()
+        r.set_camera(cam)  # the beam table recomputed (an unchanged camera would reuse it)
         t0 = time.perf_counter()
         r.render_device(p, acc.data_ptr(), None, stream)
         torch.cuda.synchronize()

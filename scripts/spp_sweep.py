@@ -16,6 +16,7 @@ acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"); acc[:, 3] = 1
 mega = "--mega" in sys.argv
 for spp in [int(x) for x in (a for a in sys.argv[2:] if not a.startswith("--"))] or [4, 16, 64, 256]:
     r.reset_stats()
+    r.set_camera(cam)  # every render recomputes the beam table (round 5 caches it for an unchanged camera)
     p = r.params(W, H, 0, spp, megakernel=mega, kernel_timing="--ktime" in sys.argv, preview="--preview" in sys.argv)
     torch.cuda.synchronize(); t = time.perf_counter()
     r.render_device(p, acc.data_ptr(), None, torch.cuda.current_stream().cuda_stream)

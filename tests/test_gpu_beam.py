@@ -1,4 +1,4 @@
-"""The camera rays' beam start (beam_kernel): each beam tile's (4x4 pixels) camera rays begin ESVO at
+"""The camera rays' beam start (beam_kernel): each beam tile's (2x2 pixels) camera rays begin ESVO at
 the distance from the eye to the nearest leaf cell inside the tile's pyramid, not at the cube entry.
 The cells skipped are empty, so a render with the beam equals the render without it (OCTPT_BEAM=0,
 itself checked against the oracle by the parity suite) bit for bit: radiance, per-pixel segment
@@ -172,7 +172,7 @@ def assert_parity_shipped(gpu, ref, tag):
 
 @pytest.mark.parametrize("name,spp", [("C3", 2), ("C4", 1), ("C5", 1), ("C5b", 1)])
 def test_beam_fullframe_oracle(torch_cuda, beam, name, spp):
-    """The shipped default (the camera rays' beam start on, 4x4 beam tiles) against the oracle over WHOLE
+    """The shipped default (the camera rays' beam start on, 2x2 beam tiles) against the oracle over WHOLE
     BASELINE-size frames (C3 1920x1080, C4 / C5 / C5b 3840x2160): the beam table's indexing at these tile
     counts and every beam start enter the comparison, not only beam == no-beam at reduced sizes."""
     from octree_pathtracing_amd import scene as S
@@ -264,3 +264,65 @@ def test_beam_step_cap(torch_cuda, renderer, beam):
                                                                        "OCTPT_CHUNK": "8192"}), sc, cam, rs)
     beam_pool_small.close()
     assert_parity_shipped(small, ref, "cap beam, small pool (regenerated camera rays)")
+
+
+def test_beam_table_reuse(torch_cuda, beam):
+    """The beam table is kept for the next render with the same scene, camera, frame size and shard (round 5): a
+    progressive continuation that does not set the camera again reuses it, and equals one with it recomputed; a
+    new camera, a new scene or another shard recomputes it (each equals a fresh context's render)."""
+    from octree_pathtracing_amd import scene as S
+
+    sc, cam, rs = S.make_config("C3")
+    W, H = 240, 136
+    stream = torch_cuda.cuda.current_stream().cuda_stream
+
+    def frame(r, spp_start, acc, shard=(0, 1)):
+        n = acc.shape[0]
+        r.render_device(r.params(W, H, spp_start, 2, shard[0], shard[1], compact=shard[1] > 1), acc.data_ptr(), None,
+                        stream)
+        torch_cuda.cuda.synchronize()
+        return acc.cpu().numpy().reshape(n, 4).copy()
+
+    def fresh_acc(n):
+        a = torch_cuda.zeros((n, 4), dtype=torch_cuda.float32, device="cuda")
+        a[:, 3] = 1.0
+        return a
+
+    beam.set_scene(sc)
+    beam.set_camera(cam)
+    beam.max_depth, beam.seed = rs.max_depth, rs.seed
+    a = fresh_acc(W * H)
+    frame(beam, 0, a)
+    reused = frame(beam, 2, a)  # same camera: the table from the first call
+    b = fresh_acc(W * H)
+    frame(beam, 0, b)
+    beam.set_camera(cam)  # recomputed
+    recomputed = frame(beam, 2, b)
+    assert np.array_equal(reused.view(np.uint32), recomputed.view(np.uint32))
+    # a new camera after a cached table: equal to a render whose table was computed for that camera alone
+    cam2 = S.Camera.look_at((60.0, 170.0, -90.0), (130.0, 120.0, 130.0))
+    beam.set_camera(cam2)
+    moved = frame(beam, 0, fresh_acc(W * H))
+    other = _renderer_with({"OCTPT_BEAM": "1"})
+    try:
+        other.set_scene(sc)
+        other.set_camera(cam2)
+        other.max_depth, other.seed = rs.max_depth, rs.seed
+        want = frame(other, 0, fresh_acc(W * H))
+        assert np.array_equal(moved.view(np.uint32), want.view(np.uint32))
+        # another shard after the whole frame's table: its own table
+        from octree_pathtracing_amd.renderer import shard_pixels
+
+        n1 = shard_pixels(W, H, 1, 3)
+        got = frame(beam, 0, fresh_acc(n1), shard=(1, 3))
+        exp = frame(other, 0, fresh_acc(n1), shard=(1, 3))
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
+        # a new scene under the same camera and shard: its own table
+        sc2 = S.make_config("C5b")[0]
+        beam.set_scene(sc2)
+        other.set_scene(sc2)
+        got = frame(beam, 0, fresh_acc(n1), shard=(1, 3))
+        exp = frame(other, 0, fresh_acc(n1), shard=(1, 3))
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
+    finally:
+        other.close()
