@@ -1021,16 +1021,21 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         // the lean 24-B path state: L stays 0 until the path ends, item = slot
         ctx->wb.lean = (!regen && ctx->lean_scene && !ctx->no_lean) ? 1u : 0u;
         const int grid_shade = grid_shade_of(shade_mode(regen, ctx->wb.lean != 0u));
+        // the seed writes its camera rays as 16-B records (store_cam_ray) when every item has its pixel: the first
+        // extend (cam) and shade (first = 2) decode them
+        const bool cam_rec = OCTPT_CAM_RECORDS && !regen && ((Rc.W | Rc.H) & (kTile - 1u)) == 0u;
         HIP_TRY(ctx, launch_wf_seed(ctx->C, Rc, B, n_seed, chunk_items, ctx->d_stats, s));
         for (uint32_t it = 0;; ++it) {
             if (cancel && cancel->load()) return fail(ctx, OCTPT_CANCELLED, "render cancelled");
             const uint32_t q = it & 1u;
             EventPair ev{};
             if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
-            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, ctx->refill, grid_extend, ctx->d_stats, s));
+            HIP_TRY(ctx, launch_wf_extend(ctx->S, B, q, it == 0u && cam_rec, ctx->refill, grid_extend,
+                                          ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 0, ev)) != OCTPT_OK) return st;
             if ((st = ktimer_begin(ctx, s, ev)) != OCTPT_OK) return st;
-            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, it == 0u, regen, grid_shade, ctx->d_stats, s));
+            HIP_TRY(ctx, launch_wf_shade(ctx->S, ctx->C, Rc, B, q, chunk_items, it == 0u ? (cam_rec ? 2u : 1u) : 0u,
+                                         regen, grid_shade, ctx->d_stats, s));
             if ((st = ktimer_end(ctx, s, 1, ev)) != OCTPT_OK) return st;
             // snapshot of the queue iteration `it` produced; the host checks the snapshot of
             // iteration it - kLookahead, so the GPU always has kLookahead iterations queued (an

@@ -21,6 +21,15 @@ constexpr uint32_t kPrimIndexMask = 0x07FFFFFFu;  // primitive indices < 2^27 (h
 #define OCTPT_BEAM_TILE 2
 #endif
 constexpr uint32_t kBeamTile = OCTPT_BEAM_TILE;
+// the seed's camera rays as 16-B records when every chunk item has its pixel (store_cam_ray; A/B knob; the
+// seed-ticket A/B build writes store_ray's records)
+#ifndef OCTPT_CAM_RECORDS
+#ifdef OCTPT_SEED_TICKET
+#define OCTPT_CAM_RECORDS 0
+#else
+#define OCTPT_CAM_RECORDS 1
+#endif
+#endif
 constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primary rays
 constexpr uint32_t kBlock = 256;       // threads per block (4 waves)
 constexpr uint32_t kMaxDepth = 21;     // new_octree.rs:14
@@ -258,12 +267,12 @@ hipError_t launch_render(const DevScene &S, const DevCamera &C, const DevRender 
                          hipStream_t stream);
 hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t n_seed,
                           uint32_t chunk_items, unsigned long long *stats, hipStream_t stream);
-hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, bool cam, uint32_t refill, int grid,
                             unsigned long long *stats, hipStream_t stream);
 // first: the chunk's first shade (the seed's rays: path state rebuilt from item0); regen: the pool is
 // smaller than the chunk, finished paths regenerate their slots (the instance with regeneration)
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
-                           uint32_t chunk_items, bool first, bool regen, int grid, unsigned long long *stats,
+                           uint32_t chunk_items, uint32_t first, bool regen, int grid, unsigned long long *stats,
                            hipStream_t stream);
 // blocks per CU of the shade instance (shade_mode; registers bound it, shade uses no dynamic LDS)
 int shade_blocks_per_cu(const DevScene &S, int mode);

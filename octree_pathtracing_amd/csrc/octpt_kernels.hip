@@ -1857,6 +1857,18 @@ __device__ __forceinline__ void store_ray(const WaveBuffers &B, uint32_t q, uint
                                  __uint_as_float(slot | (vdot(ps.d, ps.n) < 0.0f ? 0x80000000u : 0u) |
                                                  (beam ? kRayBeamBit : 0u)));
 }
+// The seed's camera rays when every chunk item has its pixel (direct seeding, OCTPT_CAM_RECORDS): 16 B, ray1
+// alone as (d, the beam start or 0); the origin is the eye, the last primitive none, and the slot the item, which
+// the position gives (shard_lo(segment) + index in it).  8.5 GB less written by the seed and read by the first
+// extend per C3 frame.  cam_ray turns one into store_ray's two records in registers.
+__device__ __forceinline__ void store_cam_ray(const WaveBuffers &B, uint32_t pos, const PathState &ps) {
+    B.ray1[0][pos] = make_float4(ps.d.x, ps.d.y, ps.d.z, ps.beam > 0.0f ? ps.beam : 0.0f);
+}
+__device__ __forceinline__ void cam_ray(float4 eye, uint32_t slot, float4 &r0, float4 &r1) {
+    const float b = r1.w;
+    r0 = make_float4(eye.x, eye.y, eye.z, b > 0.0f ? b : eye.w);  // eye.w: kPrimNone (WaveBuffers::eye)
+    r1.w = __uint_as_float(slot | (b > 0.0f ? kRayBeamBit : 0u));
+}
 // a ray record's last primitive and beam start
 __device__ __forceinline__ uint32_t ray_last_prim(float4 r0, float4 r1) {
     return (__float_as_uint(r1.w) & kRayBeamBit) ? kPrimNone : __float_as_uint(r0.w);
@@ -2064,7 +2076,12 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
         if (((R.W | R.H) & (kTile - 1u)) == 0u) {
             if (blockIdx.x == 0u && threadIdx.x < kSegs)
                 B.ctrl[ctr_count(0u, threadIdx.x)] = shard_lo(threadIdx.x + 1u, chunk_items) - shard_lo(threadIdx.x, chunk_items);
+#if OCTPT_CAM_RECORDS
+            if (ok) store_cam_ray(B, seg * B.seg_cap + (item - lo), ps);
+            if (blockIdx.x == 0u && threadIdx.x == 0u) B.ray0[0][0] = B.eye;  // the camera records' origin record
+#else
             if (ok) store_ray(B, 0u, seg * B.seg_cap + (item - lo), slot, ps);
+#endif
             // every item has its pixel (no tile overhangs the image), so the chunk starts chunk_items paths: one
             // add by block 0 instead of a counter flush per wave (8.3 M per C3 frame)
             if (blockIdx.x == 0u && threadIdx.x == 0u) atomicAdd(&stats[kStatPaths], (unsigned long long)chunk_items);
@@ -2127,6 +2144,11 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
     extern __shared__ uint2 lds_stack[];
     const Stack stk = stack_of(lds_stack, S.depth);
     const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
+    // refill bit 31 (launch_wf_extend's cam): the queue holds the seed's 16-B camera records (store_cam_ray), whose
+    // origin record (eye, kPrimNone) the seed left at ray0[0] (no LDS for it: one more LDS granule per block
+    // takes the depth-10 box instance from 7 blocks per CU to 6)
+    const bool cam = OCTPT_CAM_RECORDS && (refill >> 31) != 0u;
+    refill &= 0x7FFFFFFFu;
     if (blockIdx.x == 0 && threadIdx.x < kSegs) {  // the other queue is refilled by this iteration's shade
         B.ctrl[ctr_count(q ^ 1u, threadIdx.x)] = 0u;
         B.ctrl[ctr_head(q ^ 1u, threadIdx.x)] = 0u;
@@ -2187,10 +2209,14 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                 const uint32_t r = lanes_below(im);
                 if (r < avail) {
                     pos = seg * B.seg_cap + c_next + r;
-                    const float4 r0 = ray0[pos], r1 = ray1[pos];
+                    const float4 r1 = ray1[pos];
+                    // a camera record (cam, wave-uniform): from the eye (its w kPrimNone, so that the last
+                    // primitive decodes as none), r1.w the beam start or 0 (sign clear: not inward)
+                    const float4 r0 = ray0[cam ? 0u : pos];
+                    const float bm = cam ? r1.w : ray_beam(r0, r1);
                     tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), ray_last_prim(r0, r1),
                                         (__float_as_uint(r1.w) >> 31) != 0u);
-                    esvo_begin(S, tr, E, stk, ray_beam(r0, r1));
+                    esvo_begin(S, tr, E, stk, bm);
                     cnt.steps -= E.iter;  // a beam start's bound of skipped iterations: executed ones are counted
                 }
             }
@@ -2388,7 +2414,11 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? OCTPT_SHADE_LEAN_WAVES : OCTPT
         bool append = false, finished = false;
         PathState ps;
         if (valid) {
-            const float4 r1 = B.ray1[q][i];
+            float4 r1 = B.ray1[q][i];
+            if (first == 2u) {  // the seed's 16-B camera records: slot = item = shard_lo(seg) + index in the segment
+                float4 r0c;
+                cam_ray(B.eye, shard_lo(seg, chunk_items) + base + lane, r0c, r1);
+            }
             const float4 r0 = first ? B.eye : B.ray0[q][i];  // (the chunk's first shade: the seed's camera rays)
             append = shade_lane<kNee, kMode == 2>(S, C, R, B, first != 0u, r0, r1, B.hit + i, B.huv + i, ps, slot, item,
                                                   cnt);
@@ -2952,10 +2982,11 @@ hipError_t launch_wf_seed(const DevCamera &C, const DevRender &R, const WaveBuff
     return hipGetLastError();
 }
 
-hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, uint32_t refill, int grid,
+hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q, bool cam, uint32_t refill, int grid,
                             unsigned long long *stats, hipStream_t stream) {
-    // refill 0: the adaptive threshold
-    void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &refill, &stats};
+    // refill 0: the adaptive threshold; cam: queue q holds the seed's camera records (refill bit 31)
+    uint32_t rf = refill | (cam ? 0x80000000u : 0u);
+    void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &rf, &stats};
     const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth),
                                          stream);
     if (e != hipSuccess) return e;
@@ -2984,9 +3015,9 @@ int shade_blocks_per_cu(const DevScene &S, int mode) {
 }
 
 hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t q,
-                           uint32_t chunk_items, bool first, bool regen, int grid, unsigned long long *stats,
+                           uint32_t chunk_items, uint32_t first, bool regen, int grid, unsigned long long *stats,
                            hipStream_t stream) {
-    uint32_t first_u = first ? 1u : 0u;
+    uint32_t first_u = first;
     void *args[] = {const_cast<DevScene *>(&S), const_cast<DevCamera *>(&C), const_cast<DevRender *>(&R),
                     const_cast<WaveBuffers *>(&B), &q, &chunk_items, &first_u, &stats};
     const hipError_t e = hipLaunchKernel(shade_instance(S, shade_mode(regen, B.lean != 0u)), dim3(grid), dim3(kBlock),
