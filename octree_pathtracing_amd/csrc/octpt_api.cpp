@@ -35,7 +35,7 @@ constexpr uint64_t kDefaultChunkPaths = 1ull << 29;  // 4K: 64-spp chunks (C5 46
 #define OCTPT_LOOKAHEAD 3
 #endif
 constexpr uint32_t kLookahead = OCTPT_LOOKAHEAD;    // host steering: iterations queued ahead of the check
-constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (116 B each: queues + path state)
+constexpr uint32_t kDefaultPool = 512u << 20;        // path slots in flight (124 B each: queues + path state)
 constexpr uint32_t kMaxPool = 1u << 30;              // the sun-sampling planes index 4 * pool slots in uint32
 constexpr uint32_t kMinPool = 1u << 20;              // floor of the out-of-memory fallback (halving)
 constexpr uint64_t kMaxBuildPairs = 1ull << 31;      // octree builder: (cell, primitive) pair cap
@@ -793,7 +793,7 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
         HIP_TRY(ctx, hipDeviceSynchronize());
         free_queues(ctx);
         WaveBuffers &B = ctx->wb;
-        // queues + path state: 116 B per slot
+        // queues + path state: 124 B per slot
         size_t want = pool;
         for (;;) {
             B.seg_cap = (uint32_t)seg_cap_for(want);
@@ -802,9 +802,10 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.ray0[1]);
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.ray1[0]);
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.ray1[1]);
-            if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pa);
-            if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pb);
-            if (e == hipSuccess) e = wave_alloc(ctx, want, &B.pc);
+            // pa, pb: per slot, or (the lean state) per position of queue 0 / 1; pc: per slot, or both queues
+            if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.pa);
+            if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.pb);
+            if (e == hipSuccess) e = wave_alloc(ctx, 2 * qlen, &B.pc);
             if (e == hipSuccess) e = wave_alloc(ctx, want, &B.item0);
             if (e == hipSuccess) e = wave_alloc(ctx, qlen, &B.hit);
             if (e == hipSuccess) e = wave_alloc(ctx, kCtrlWords, &B.ctrl);

@@ -1902,6 +1902,21 @@ __device__ __forceinline__ void store_path(const WaveBuffers &B, uint32_t slot, 
     B.pc[slot] = c;
 }
 
+// The lean state travels with its ray (OCTPT_LEAN_POS, round 5): shade stores it at the continuing ray's queue
+// position (queue q: (T, rng) in pa for q = 0, pb for q = 1 -- pb is free in the lean state -- and (cur, bits) in
+// pc's half q), so the next shade reads it at the position it reads the ray and hit records at, coalesced and
+// without waiting for the ray record's slot word.
+#ifndef OCTPT_LEAN_POS
+#define OCTPT_LEAN_POS 1
+#endif
+__device__ __forceinline__ void store_lean_at(const WaveBuffers &B, uint32_t q, uint32_t pos, const PathState &ps) {
+    float4 a, b;
+    uint2 c;
+    pack_path(ps, 0u, a, b, c);
+    (q ? B.pb : B.pa)[pos] = make_float4(a.x, a.y, a.z, b.z);
+    B.pc[(size_t)q * kSegs * B.seg_cap + pos] = c;
+}
+
 // sun-sampling state of a slot (kNee): the waiting bounce + mult, and the attenuation
 __device__ __forceinline__ void store_nee(const WaveBuffers &B, uint32_t slot, const PathState &ps) {
     B.pd[slot] = make_float4(ps.co.x, ps.co.y, ps.co.z, __uint_as_float(ps.clast));
@@ -2285,11 +2300,14 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
 // it finished (its colour record written).  first (wave-uniform: the chunk's first shade, whose
 // rays the seed started): the path state is rebuilt from the slot's item as the seed computed it,
 // through the same pack / unpack as a stored path, instead of being read.
+// kLean with OCTPT_LEAN_POS: the state is read at (q, pos) and a continuing path's is not stored here: the caller
+// stores it at the position its next ray takes (store_lean_at).
 template <bool kNee, bool kLean = false>
 __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C, const DevRender &R,
                                            const WaveBuffers &B, bool first, float4 r0, float4 r1, const uint2 *hit_rec,
                                            const float2 *huv_rec, PathState &ps, uint32_t &slot, uint32_t &item,
-                                           Counters &cnt) {
+                                           Counters &cnt, uint32_t q = 0u, uint32_t pos = 0u) {
+    constexpr bool kPos = kLean && OCTPT_LEAN_POS;
     slot = __float_as_uint(r1.w) & (kRayBeamBit - 1u);
     if (first) {
         item = kLean ? slot : B.item0[slot];
@@ -2299,6 +2317,10 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
         uint2 c;
         pack_path(s0, item, a, b, c);
         unpack_path(a, b, c, B.eye, r1, ps, item);  // a camera ray's ray0 is (eye, kPrimNone): not re-read
+    } else if constexpr (kPos) {  // L = +0 as the path started, item = slot (store_lean_at)
+        const float4 a = (q ? B.pb : B.pa)[pos];
+        unpack_path(make_float4(a.x, a.y, a.z, 0.0f), make_float4(0.0f, 0.0f, a.w, __uint_as_float(slot)),
+                    B.pc[(size_t)q * kSegs * B.seg_cap + pos], r0, r1, ps, item);
     } else {
         load_path<kLean>(B, slot, r0, r1, ps, item);
     }
@@ -2307,7 +2329,7 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
         // a beam-started camera ray that reached the reference's step cap (extend's kHitCapped record): the
         // same ray is queued again without its beam start, for the walk from the cube entry.  No segment
         // is counted; the path state is the seed's (stored now when this shade rebuilt it from the item).
-        if (first) store_path<kLean>(B, slot, ps, item);
+        if (first && !kPos) store_path<kLean>(B, slot, ps, item);
         ps.n = V(0.0f, 0.0f, 0.0f);
         ps.beam = 0.0f;
         cnt.redo++;
@@ -2333,7 +2355,7 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     bool cont = shade_segment<kNee>(S, R, ps, hit, cnt);
     if (cont) cont = begin_segment(ps);
     if (cont) {
-        store_path<kLean>(B, slot, ps, item);
+        if (!kPos) store_path<kLean>(B, slot, ps, item);
         if (kNee && ps.shadow) {  // a shadow segment follows: new sun sample or the next one
             if (!was_shadow) store_nee(B, slot, ps);
             store_att(B, slot, ps);
@@ -2421,7 +2443,7 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? OCTPT_SHADE_LEAN_WAVES : OCTPT
             }
             const float4 r0 = first ? B.eye : B.ray0[q][i];  // (the chunk's first shade: the seed's camera rays)
             append = shade_lane<kNee, kMode == 2>(S, C, R, B, first != 0u, r0, r1, B.hit + i, B.huv + i, ps, slot, item,
-                                                  cnt);
+                                                  cnt, q, i);
             finished = !append;
         }
         // regenerate: finished lanes take the next chunk items (path regeneration)
@@ -2429,7 +2451,10 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? OCTPT_SHADE_LEAN_WAVES : OCTPT
             if (regen(C, R, B, slot, finished, chunk_items, cur, ps, cnt)) append = true;
         }
         const uint32_t t = wave_ticket(B.ctrl + ctr_count(q ^ 1u, seg), append);
-        if (append) store_ray(B, q ^ 1u, seg0 + t, slot, ps);
+        if (append) {
+            store_ray(B, q ^ 1u, seg0 + t, slot, ps);
+            if constexpr (kMode == 2 && OCTPT_LEAN_POS) store_lean_at(B, q ^ 1u, seg0 + t, ps);
+        }
     }
     cnt.ib = 0u;  // issued bytes are extend's only
     flush_counters(cnt, stats);
@@ -2455,7 +2480,8 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
     for (uint32_t k = 0; k < kSegs; ++k) {  // queue q, segment after segment, dealt over the waves
         const uint32_t n = min(B.ctrl[ctr_count(q, k)], jlim);
         for (uint32_t j = wid; j < n; j += nw) {
-            float4 r0 = B.ray0[q][k * B.seg_cap + j], r1 = B.ray1[q][k * B.seg_cap + j];
+            const uint32_t p = k * B.seg_cap + j;
+            float4 r0 = B.ray0[q][p], r1 = B.ray1[q][p];
             for (;;) {
                 const TraceRay tr = make_trace_ray(S, V(r0.x, r0.y, r0.z), V(r1.x, r1.y, r1.z), ray_last_prim(r0, r1),
                                                    (__float_as_uint(r1.w) >> 31) != 0u);
@@ -2489,10 +2515,13 @@ __global__ __launch_bounds__(kBlock) void wf_drain_kernel(DevScene S, DevRender 
                 const float2 huv = make_float2(h.u, h.v);
                 PathState ps;
                 uint32_t slot, item;
-                const bool cont = (!kNee && B.lean)
-                                      ? shade_lane<kNee, true>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item, cnt)
-                                      : shade_lane<kNee, false>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item, cnt);
+                const bool lean = !kNee && B.lean;
+                const bool cont = lean ? shade_lane<kNee, true>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item,
+                                                                cnt, q, p)
+                                       : shade_lane<kNee, false>(S, DevCamera{}, R, B, false, r0, r1, &hr, &huv, ps, slot, item, cnt);
                 if (!cont) break;
+                // the lean state back at this path's queue position, where its next shade_lane reads it
+                if (OCTPT_LEAN_POS && lean) store_lean_at(B, q, p, ps);
                 // the next segment's ray record, as store_ray writes it
                 r0 = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.last_prim));
                 r1 = make_float4(ps.d.x, ps.d.y, ps.d.z,
