@@ -2150,7 +2150,7 @@ constexpr uint32_t kClaim = OCTPT_CLAIM;
 #define OCTPT_THR_SHORT 32  // ... and with short rays
 #endif
 #ifndef OCTPT_SHORT_STEPS
-#define OCTPT_SHORT_STEPS 56  // mean ESVO steps below which a wave's rays count as short (A/B knob)
+#define OCTPT_SHORT_STEPS 48  // mean ESVO steps below which a wave's rays count as short (A/B knob; round 5: 56 -> 48)
 #endif
 constexpr uint32_t kShortRaySteps = OCTPT_SHORT_STEPS;
 template <int kPrims>
