@@ -18,6 +18,7 @@
 #   run:CMD               any command (no colons in it), e.g. "python3 scripts/stale_hit_probe.py slotleak_check"
 #                                                                                 -> run_<n>.log
 #   ab:CFG/SPP,...:LIB,...  scripts/ab.sh A/B of library builds ("cur" = the in-tree library) -> ab_<n>.txt
+#   abenv:CFG/SPP,...:VAR+VAR  scripts/ab_env.sh A/B of builds and env settings (VAR = LIB or LIB|ENV=V,ENV=V) -> ab_<n>.txt
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -77,6 +78,10 @@ for task in "$@"; do
       cat $O/bench_n8_gloo.json ;;
     ab)
       timeout -k 10 1000 bash scripts/ab.sh "$(echo ${a//,/ } | tr / :)" ${b//,/ } > $O/ab_$n.txt 2>&1 || fail "$task" $O/ab_$n.txt
+      cat $O/ab_$n.txt ;;
+    abenv)  # abenv:CFG/SPP,...:VAR+VAR+...  (VAR = LIB or LIB|ENV=V,ENV2=V; scripts/ab_env.sh)
+      IFS=+ read -r -a VARS <<< "$b"
+      timeout -k 10 1000 bash scripts/ab_env.sh "$(echo ${a//,/ } | tr / :)" "${VARS[@]}" > $O/ab_$n.txt 2>&1 || fail "$task" $O/ab_$n.txt
       cat $O/ab_$n.txt ;;
     run) timeout -k 10 600 bash -c "$a" > $O/run_$n.log 2>&1 || fail "$task" $O/run_$n.log; tail -5 $O/run_$n.log ;;
     *) fail "unknown task $task" ;;
