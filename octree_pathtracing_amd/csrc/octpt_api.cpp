@@ -152,6 +152,8 @@ struct octpt_ctx {
                    h == o.h && shard_index == o.shard_index && shard_count == o.shard_count;
         }
     } beam_key;
+    // recorded on the stream that computed the table: a render on another stream that reuses it waits for it
+    hipEvent_t beam_ev = nullptr;
 };
 
 struct octpt_frame {
@@ -992,10 +994,14 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
             HIP_TRY(ctx, hipMalloc(&ctx->d_beam, n_tiles * sizeof(float)));
             ctx->beam_cap = n_tiles;
         }
+        if (!ctx->beam_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->beam_ev, hipEventDisableTiming));
         if (!(key == ctx->beam_key)) {  // same scene, camera, size, shard and deal: the table is already there
             ctx->beam_key.valid = false;
             HIP_TRY(ctx, launch_beam(ctx->S, ctx->C, R, ctx->d_beam, s));
+            HIP_TRY(ctx, hipEventRecord(ctx->beam_ev, s));
             ctx->beam_key = key;
+        } else {
+            HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->beam_ev, 0));  // (a no-op on the stream that computed it)
         }
         beam = ctx->d_beam;
     }
@@ -1526,6 +1532,7 @@ void octpt_destroy(octpt_ctx *ctx) {
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_subs) (void)hipFree(ctx->d_subs);
     if (ctx->d_beam) (void)hipFree(ctx->d_beam);
+    if (ctx->beam_ev) (void)hipEventDestroy(ctx->beam_ev);
     if (ctx->d_order) (void)hipFree(ctx->d_order);
     if (ctx->d_order_pos) (void)hipFree(ctx->d_order_pos);
     if (ctx->m_acc) (void)hipFree(ctx->m_acc);

@@ -276,10 +276,10 @@ def test_beam_table_reuse(torch_cuda, beam):
     W, H = 240, 136
     stream = torch_cuda.cuda.current_stream().cuda_stream
 
-    def frame(r, spp_start, acc, shard=(0, 1)):
+    def frame(r, spp_start, acc, shard=(0, 1), on=None):
         n = acc.shape[0]
         r.render_device(r.params(W, H, spp_start, 2, shard[0], shard[1], compact=shard[1] > 1), acc.data_ptr(), None,
-                        stream)
+                        on or stream)
         torch_cuda.cuda.synchronize()
         return acc.cpu().numpy().reshape(n, 4).copy()
 
@@ -293,7 +293,9 @@ def test_beam_table_reuse(torch_cuda, beam):
     beam.max_depth, beam.seed = rs.max_depth, rs.seed
     a = fresh_acc(W * H)
     frame(beam, 0, a)
-    reused = frame(beam, 2, a)  # same camera: the table from the first call
+    # same camera: the table from the first call, reused on another stream (which waits for the table's event)
+    side = torch_cuda.cuda.Stream()
+    reused = frame(beam, 2, a, on=side.cuda_stream)
     b = fresh_acc(W * H)
     frame(beam, 0, b)
     beam.set_camera(cam)  # recomputed
