@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--balance", action="store_true")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="render each shard through one context of this many entries on device 0 (octpt_create_multi: "
+                         "the shard's tiles split again over concurrent wavefronts on the one GPU)")
     args = ap.parse_args()
     import torch
     from octree_pathtracing_amd import scene as S
@@ -32,11 +35,12 @@ def main():
     if args.spp:
         rs.spp = args.spp
     W, H = rs.width, rs.height
-    r = HipRenderer(device=0)
+    r = HipRenderer(devices=[0] * args.lanes) if args.lanes > 1 else HipRenderer(device=0)
     r.set_scene(sc)
     r.set_camera(cam)
     r.max_depth, r.seed = rs.max_depth, rs.seed
-    out = {"config": args.config, "spp": rs.spp, "deal": "balanced" if args.balance else "round robin", "runs": {}}
+    out = {"config": args.config, "spp": rs.spp, "deal": "balanced" if args.balance else "round robin", "lanes": args.lanes,
+           "runs": {}}
     stream = torch.cuda.current_stream().cuda_stream
     seg_full = None
     if args.balance:  # the one-GPU frame's per-pixel segment counts, the cost the balanced deal evens out
