@@ -930,6 +930,10 @@ __device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uin
 #ifndef OCTPT_FOLD
 #define OCTPT_FOLD 1  // absent-sibling folds per step (A/B: -DOCTPT_FOLD=0)
 #endif
+#ifndef OCTPT_FOLD_SPHERES
+// the sphere instance folds up to 2 (round 5: C3 +0.4 %; the box instance stays at 1: 2 folds there C4 -2.2 %)
+#define OCTPT_FOLD_SPHERES 2
+#endif
 #ifndef OCTPT_FOLD_MODELS
 // the block-model instance folds up to 2 (C5, depth-11 voxel terrain: +1.9 %; 2 folds everywhere:
 // C3 -2.4 %, C4 -2.9 %, C2 +-0)
@@ -1170,7 +1174,9 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // tests), so the wave does not pay a whole loop iteration for it.  44 % of C3's iterations are
     // such advances; folding the first of each run leaves 72 % of the iterations (tools/esvo_trace.py).
     // A fold that leaves the parent pops below, exactly as that iteration would.
-    constexpr int kFolds = kPrims == kPrimsModels ? OCTPT_FOLD_MODELS : kPrims == kPrimsBlocks ? OCTPT_FOLD_BLOCKS : OCTPT_FOLD;
+    constexpr int kFolds = kPrims == kPrimsModels ? OCTPT_FOLD_MODELS
+                           : kPrims == kPrimsBlocks ? OCTPT_FOLD_BLOCKS
+                           : kPrims == kPrimsSpheres ? OCTPT_FOLD_SPHERES : OCTPT_FOLD;
 #pragma unroll
     for (int k = 0; k < kFolds; ++k) {  // kFolds folds at most per step
     const bool fold = !leaf_hit & !stopped & !pop & (((E.pmask >> (E.idx ^ E.mirror)) & 1u) == 0u) &
