@@ -24,6 +24,7 @@ sample with the host's CPU share of threads (model, nproc and flags recorded).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -93,20 +94,46 @@ def pmc_name(config: str, world: int = 1) -> str:
     return f"pmc_{config}.json" if world == 1 else f"pmc_{config}_n{world}.json"
 
 
-def load_traffic(config: str, world: int = 1):
-    """(bytes per extend launch, source description, L2 hit rate) from the profile pmc_name(config, world)
-    names, or (None, reason, None): a line at N ranks never quotes a profile taken at another N."""
+def load_pmc(config: str, world: int = 1):
+    """(the wf_extend_kernel record, source description) of the profile pmc_name(config, world) names, or
+    (None, reason): a line at N ranks never quotes a profile taken at another N."""
     name = pmc_name(config, world)
     p = ROOT / "profiles" / name
     if p.exists():
         try:
             d = json.loads(p.read_text())
-            ext = d.get("wf_extend_kernel", {})
-            return ext.get("bytes_per_launch"), f"profiles/{name}: {d.get('correction', '')}", \
-                ext.get("l2_hit_rate")
+            return d.get("wf_extend_kernel", {}), f"profiles/{name}: {d.get('correction', '')}"
         except Exception as e:
-            return None, f"profiles/{name} unreadable ({type(e).__name__})", None
-    return None, f"no PMC profile of {config} at {world} rank(s) (profiles/{name})", None
+            return None, f"profiles/{name} unreadable ({type(e).__name__})"
+    return None, f"no PMC profile of {config} at {world} rank(s) (profiles/{name})"
+
+
+def load_traffic(config: str, world: int = 1):
+    """(bytes per extend launch, source description, L2 hit rate) from the profile pmc_name(config, world)
+    names, or (None, reason, None)."""
+    ext, src = load_pmc(config, world)
+    if ext is None:
+        return None, src, None
+    return ext.get("bytes_per_launch"), src, ext.get("l2_hit_rate")
+
+
+def measured_rates(config: str, world: int, ext_s: float):
+    """BASELINE.json's "achieved HBM GB/s" as rocprof measures it: the same-N profile's FETCH_SIZE (read) and
+    WRITE_SIZE (write) bytes per wf_extend_kernel launch (L2-to-fabric requests, Infinity-Cache hits included,
+    so an upper bound of HBM bytes; rank 0's shard at N > 1) over this run's mean extend launch duration on the
+    same rank, each as a fraction of one GPU's HBM peak.  None without a same-N profile."""
+    ext, src = load_pmc(config, world)
+    if not ext or ext_s <= 0 or "fetch_bytes_per_launch" not in ext:
+        return None
+    rd, wr = ext["fetch_bytes_per_launch"] / ext_s / 1e9, ext["write_bytes_per_launch"] / ext_s / 1e9
+    return {"read_gbs": round(rd, 1), "read_frac": round(rd / HBM_PEAK_GBS, 4),
+            "write_gbs": round(wr, 1), "write_frac": round(wr / HBM_PEAK_GBS, 4),
+            "total_gbs": round(rd + wr, 1), "total_frac": round((rd + wr) / HBM_PEAK_GBS, 4),
+            "l2_hit_rate": ext.get("l2_hit_rate"), "launches_profiled": ext.get("launches"),
+            "source": src.split(":")[0],
+            "basis": "rocprofv3 FETCH_SIZE / WRITE_SIZE bytes per extend launch of the same-N profile (rank 0's "
+                     "shard at N > 1) / this run's mean extend launch duration on rank 0 (HIP events); fabric "
+                     "bytes, Infinity-Cache hits included: an upper bound of HBM traffic"}
 
 
 def roofline_over_ranks(ranks: list) -> dict:
@@ -303,6 +330,20 @@ def balance_deal(r, segbuf, n_local: int, W: int, H: int, rank: int, world: int,
     return "balanced: octpt_balance_tiles over the warmup step's per-tile segment counts"
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """fd 1 redirected to fd 2 for the block (output printed by native code, which sys.stdout does not see)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def scene_contents(sc) -> str:
     if sc.blocks is not None:  # block-value leaves (DESIGN.md C23)
         return f"{len(sc.cells)} voxel cells as block-value leaves ({len(sc.blocks)} block kinds)"
@@ -334,7 +375,8 @@ def main():
                          "measured equal on C3 / C5b, so round robin stays the default)")
     ap.add_argument("--no-capi-multi", action="store_true",
                     help="with N > 1 ranks, skip rank 0's extra measurement of the same frame through one "
-                         "multi-device context over the N devices")
+                         "multi-device context over the N devices (after the timed steps; the other ranks wait on a "
+                         "gloo group, so no RCCL kernel sits on the GPUs it renders on)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -358,11 +400,17 @@ def main():
         sys.exit(2)
     dev_idx = local % max(n_dev, 1)
     torch.cuda.set_device(dev_idx)
+    host_group = None
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
-        else:
-            dist.init_process_group("gloo")
+        # gloo prints "[Gloo] Rank r is connected to ..." on stdout from C++ while it connects: stdout carries the
+        # bench's one JSON line, so the connects run with fd 1 pointed at stderr
+        with stdout_to_stderr():
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+            else:
+                dist.init_process_group("gloo")
+            # rank 0's extra legs after the timed steps are waited for on this host-side group (below)
+            host_group = dist.new_group(backend="gloo")
         assert dist.get_world_size() == args.gpus
 
     from octree_pathtracing_amd import scene as S
@@ -372,8 +420,11 @@ def main():
     sc, cam, rs = S.make_config(args.config, build=not args.compact)
     if args.compact:
         sc.build_octree(sc._depth, compact=True)
+    spp_default = rs.spp
     if args.spp:
         rs.spp = args.spp
+    # a committed PMC profile is of the config's own frame: a run at another spp (other launches) quotes none
+    pmc_ok = rs.spp == spp_default and not args.compact
     W, H = rs.width, rs.height
     multi = capi_devices(args.capi_devices, n_dev) if (args.capi_devices and world == 1) else None
     r = HipRenderer(devices=multi) if multi else HipRenderer(device=dev_idx)
@@ -451,7 +502,8 @@ def main():
     sh_s = st["shade_ms"] / 1e3 / n_sh
     lean = lean_state(sc, st)
     sh_bytes = shade_bytes(st, lean, shade_lds_tables(sc)) / n_sh
-    traffic, traffic_src, l2_hit = load_traffic(args.config, world)
+    traffic, traffic_src, l2_hit = load_traffic(args.config, world) if pmc_ok else \
+        (None, f"the committed profiles are of {args.config}'s own frame ({spp_default} spp, full octree)", None)
     out = {
         "metric": METRIC,
         "value": round(seg / dt / 1e6, 2),
@@ -513,24 +565,31 @@ def main():
         out["roofline"]["achieved_basis"] = "mean over ranks of each rank's extend bytes / its extend time"
     if multi:
         out["config"]["capi_devices"] = multi
+    out["roofline"]["measured"] = measured_rates(args.config, world, ext_s) if pmc_ok else None
+    # After the timed steps and the gather, rank 0 alone runs the extra legs (the C-ABI multi-device frame, the
+    # CPU baseline) while the other ranks wait on a gloo group: a wait on the RCCL group would leave an RCCL kernel
+    # resident on the GPUs the multi-device leg renders on.
     if world > 1 and not args.no_capi_multi:
         # the same frame through the C-ABI path a Rust host calls: one process (rank 0), one multi-device
-        # context over the N devices, tiles gathered inside liboctpt; the other ranks wait.
-        # (gloo rehearsals of N ranks on fewer GPUs repeat device ids, as the ranks do)
-        dist.barrier()
+        # context over the N devices, tiles gathered inside liboctpt.  (gloo rehearsals of N ranks
+        # on fewer GPUs repeat device ids, as the ranks do)
         if rank == 0:
             try:
                 devs = [i % max(n_dev, 1) for i in range(world)]
                 out["capi_multi"] = capi_multi_measure(sc, cam, rs, devs, args.steps, args.warmup)
             except Exception as e:  # reported, never fatal to the bench line
                 out["capi_multi"] = {"error": f"{type(e).__name__}: {e}"}
-        dist.barrier()
+        dist.barrier(group=host_group)
     if rank == 0 and world == 1 and not args.no_issued and not multi:
         out["roofline"]["issued"] = issued_probe(sc, cam, rs, dev_idx, ext_s)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # the reference's CPU path timed in the same run next to the N-GPU figure (north_star), on rank 0 only
+    if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sc, cam, rs, args.cpu_seconds, args.cpu_threads)
+        out["cpu_baseline"]["gpu_over_cpu"] = round(out["value"] / max(out["cpu_baseline"]["value"], 1e-9), 1)
     else:
         out["cpu_baseline"] = None
+    if world > 1:
+        dist.barrier(group=host_group)
     if rank == 0:
         print(json.dumps(out), flush=True)
         if args.dump_frame:  # the frame in image order (a single rank's buffer is tile-major too)

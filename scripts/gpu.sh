@@ -15,6 +15,7 @@
 #   sq:CFG                the SQ counter pass of the one-step bench                 -> sq_CFG/
 #   shard:CFG[:NS]        scripts/shard_emulation.py (NS = "1_2_4_8", the default)  -> shard_CFG.json
 #   n8                    bench.py --gpus 8 --dist-backend gloo (the driver's N = 8 command on one GPU)
+#   nrank:N[:CFG[:STEPS]] the same at N ranks with the CPU baseline, wall time recorded -> nrank_N_CFG.json/.time
 #   run:CMD               any command (no colons in it), e.g. "python3 scripts/stale_hit_probe.py slotleak_check"
 #                                                                                 -> run_<n>.log
 #   ab:CFG/SPP,...:LIB,...  scripts/ab.sh A/B of library builds ("cur" = the in-tree library) -> ab_<n>.txt
@@ -76,6 +77,13 @@ for task in "$@"; do
       timeout -k 10 600 python3 bench.py --gpus 8 --dist-backend gloo --steps 2 --warmup 1 --no-cpu-baseline \
           > $O/bench_n8_gloo.json 2> $O/bench_n8_gloo.err || fail "$task" $O/bench_n8_gloo.err
       cat $O/bench_n8_gloo.json ;;
+    nrank)  # nrank:N[:CFG[:STEPS]]: the driver's N-rank command as gloo ranks time-sharing this GPU, CPU baseline
+            # included; the command's wall time goes to nrank_N_CFG.time
+      t0=$(date +%s.%N)
+      timeout -k 10 900 python3 bench.py --gpus $a --config ${b:-C3} --dist-backend gloo --steps ${c:-2} --warmup 1 \
+          > $O/nrank_${a}_${b:-C3}.json 2> $O/nrank_${a}_${b:-C3}.err || fail "$task" $O/nrank_${a}_${b:-C3}.err
+      echo "{\"command\": \"python3 bench.py --gpus $a --config ${b:-C3} --dist-backend gloo --steps ${c:-2} --warmup 1\", \"wall_s\": $(python3 -c "print(round($(date +%s.%N) - $t0, 1))")}" > $O/nrank_${a}_${b:-C3}.time
+      cat $O/nrank_${a}_${b:-C3}.time; tail -c 600 $O/nrank_${a}_${b:-C3}.json ;;
     ab)
       timeout -k 10 1000 bash scripts/ab.sh "$(echo ${a//,/ } | tr / :)" ${b//,/ } > $O/ab_$n.txt 2>&1 || fail "$task" $O/ab_$n.txt
       cat $O/ab_$n.txt ;;
