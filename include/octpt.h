@@ -15,10 +15,11 @@
  *    the caller until octpt_frame_release.
  *  - There is no CPU fallback: without a usable gfx950 device octpt_create fails
  *    with OCTPT_ERR_DEVICE.
- *  - "Drop-in" is not literal: a Rust host binding this header adds two accessors to the reference
- *    (Octant::raw_parts in src/octree/new_octree.rs, Sun::octpt_args in src/scene/mod.rs) and supplies the
- *    block table (block value -> face materials / model) that its resource manager resolves and Scene does
- *    not hold.  src/app and the rest of src/scene are untouched.
+ *  - "Drop-in": src/octree is used unchanged (the raw octant masks come from Octant's public is_child /
+ *    is_leaf / get_child).  A Rust host binding this header adds one accessor to the
+ *    reference, Sun::octpt_args in src/scene/mod.rs (Sun's texture, colour and draw flag are private), and
+ *    supplies the block table (block value -> face materials / model) that its resource manager resolves and
+ *    Scene does not hold.  src/app and the rest of src/scene are untouched.
  */
 #ifndef OCTPT_H
 #define OCTPT_H
@@ -348,7 +349,9 @@ octpt_status octpt_balance_tiles(uint32_t width, uint32_t height, uint32_t shard
  * (octree_traversal.rs:54-302) restored.  rays: n*6 floats (origin, unit direction), host.  ESVO's
  * 1 / -|d| is exact for direction components up to 2^126 (components below 2^-23 are clamped to it as
  * the reference does); a ray with a non-finite component or a direction component above 2^126 is
- * reported as a miss, as the reference's Scene::hit reports it, and the rest of the batch is traced.
+ * reported as a miss and the rest of the batch is traced.  For a non-finite ray that is the reference's
+ * result; for a finite component above 2^126 it is a deliberate deviation (the reference's walk runs on a
+ * subnormal t_coef, octree_traversal.rs:95, and may hit; parity unpinned).
  * last_prim / last_normal (nullable): self-intersection key per ray.
  * Outputs (host): t (world, +inf on miss), prim (0xFFFFFFFF on miss; in a block-value scene, C23, the
  * block id, or 0x40000000 | quad for a block model's quad), normal n*3 (nullable), esvo steps (nullable). */

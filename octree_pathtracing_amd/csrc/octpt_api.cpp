@@ -154,6 +154,8 @@ struct octpt_ctx {
     } beam_key;
     // recorded on the stream that computed the table: a render on another stream that reuses it waits for it
     hipEvent_t beam_ev = nullptr;
+    hipStream_t beam_stream = nullptr;  // the stream the valid table was computed on
+    bool beam_shared = false;           // ... and whether a render on another stream has read it since
 };
 
 struct octpt_frame {
@@ -277,9 +279,37 @@ hipError_t upload(octpt_ctx *ctx, const T *src, size_t n, T **dst) {
     } else {
         e = hipMemset(p, 0, bytes);
         if (e != hipSuccess) return e;
+        // hipMemset runs on the null stream, which does not order itself with the context's non-blocking stream:
+        // the kernels that fill these tables on ctx->stream (fill_scene_gpu, build_ancestors_gpu) must not race it
+        e = hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) return e;
     }
     *dst = static_cast<T *>(p);
     return hipSuccess;
+}
+
+// OCTPT_STACKLESS builds: the ancestor table the stackless pop reads (DevScene::anc, build_ancestors_gpu), one
+// row of depth - 1 entries per node_child index; a scene-lifetime allocation like the other tables
+octpt_status build_ancestor_table(octpt_ctx *ctx, DevScene &S, size_t n_slots) {
+    S.anc = nullptr;
+    if (!OCTPT_STACKLESS) return OCTPT_OK;
+    const size_t row = S.depth > 1u ? S.depth - 1u : 1u;
+    if ((n_slots + 8) * row >= (1ull << 29))  // the kernel forms 32-bit byte offsets into the table
+        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "octree too large for the stackless build's ancestor table");
+    uint2 *anc = nullptr;
+    HIP_TRY(ctx, upload<uint2>(ctx, nullptr, std::max<size_t>((n_slots + 8) * row, 8), &anc));  // zeroed
+    uint2 *f = nullptr;
+    uint32_t *d_n = nullptr;
+    const size_t nf = std::max<uint32_t>(S.n_octants, 1u);
+    HIP_TRY(ctx, hipMalloc(&f, 2 * nf * sizeof(uint2)));
+    hipError_t e = hipMalloc(&d_n, sizeof(uint32_t));
+    if (e == hipSuccess) e = build_ancestors_gpu(S, anc, f, f + nf, d_n, ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(f);
+    if (d_n) (void)hipFree(d_n);
+    if (e != hipSuccess) return hip_fail(ctx, e, "ancestor table");
+    S.anc = anc;
+    return OCTPT_OK;
 }
 
 // memoised subtree height with cycle detection; returns -1 on a cycle or bad index.
@@ -744,7 +774,7 @@ void free_queues(octpt_ctx *ctx) {
     for (void *p : ctx->wave_allocs) wave_free(ctx, p);
     ctx->wave_allocs.clear();
     ctx->pool = 0;
-    ctx->wb.huv = nullptr;  // allocated with the queues (block-value scenes)
+    ctx->wb.hit4 = nullptr;  // allocated with the queues (block-value scenes)
 }
 
 void free_wave(octpt_ctx *ctx) {
@@ -830,9 +860,9 @@ octpt_status ensure_wave(octpt_ctx *ctx, size_t pool, size_t color_items, bool n
         ctx->pool = want;
         ctx->wave_allocs_n++;
     }
-    // block-value scenes (C23): the hit records' (u, v), one per queue position, with the queues
-    if (blocks && !ctx->wb.huv) {
-        const hipError_t e = wave_alloc(ctx, (size_t)kSegs * ctx->wb.seg_cap, &ctx->wb.huv);
+    // block-value scenes (C23): their 16-B hit records (t, u, v beside the block), one per queue position
+    if (blocks && !ctx->wb.hit4) {
+        const hipError_t e = wave_alloc(ctx, (size_t)kSegs * ctx->wb.seg_cap, &ctx->wb.hit4);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             *part = kOomNee;  // a per-slot plane like the sun-sampling ones: the pool shrinks
@@ -996,12 +1026,18 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         }
         if (!ctx->beam_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->beam_ev, hipEventDisableTiming));
         if (!(key == ctx->beam_key)) {  // same scene, camera, size, shard and deal: the table is already there
+            // overwriting a valid table: renders on other streams may still read it (write-after-read),
+            // so the device drains first; a render on the computing stream is ordered by the stream itself
+            if (ctx->beam_key.valid && (s != ctx->beam_stream || ctx->beam_shared)) HIP_TRY(ctx, hipDeviceSynchronize());
             ctx->beam_key.valid = false;
             HIP_TRY(ctx, launch_beam(ctx->S, ctx->C, R, ctx->d_beam, s));
             HIP_TRY(ctx, hipEventRecord(ctx->beam_ev, s));
             ctx->beam_key = key;
+            ctx->beam_stream = s;
+            ctx->beam_shared = false;
         } else {
             HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->beam_ev, 0));  // (a no-op on the stream that computed it)
+            ctx->beam_shared |= s != ctx->beam_stream;  // read on another stream: a recompute drains the device
         }
         beam = ctx->d_beam;
     }
@@ -1627,6 +1663,8 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.n_octants = d->octant_count;
         st = upload_tables(ctx, d, true, S);
         if (st != OCTPT_OK) return st;
+        st = build_ancestor_table(ctx, S, n_slots);
+        if (st != OCTPT_OK) return st;
         ctx->S = S;
         ctx->has_scene = true;
         ++ctx->scene_gen;
@@ -1703,6 +1741,8 @@ octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *d,
         S.root_mask = root_mask;
         S.n_octants = t.n_octants;
         st = upload_tables(ctx, d, false, S);
+        if (st != OCTPT_OK) return st;
+        st = build_ancestor_table(ctx, S, n_slots);
         if (st != OCTPT_OK) return st;
         ctx->S = S;
         ctx->has_scene = true;
@@ -1919,9 +1959,33 @@ octpt_status octpt_set_tile_order(octpt_ctx *ctx, uint32_t width, uint32_t heigh
     if (!ctx) return OCTPT_ERR_INVALID_ARG;
     join_inflight(ctx);
     try {
-        for (octpt_ctx *c : ctx->sub) {  // every device entry deals the same way (its sub-shards nest in it)
-            const octpt_status st = octpt_set_tile_order(c, width, height, order);
-            if (st != OCTPT_OK) return fail(ctx, st, c->err);
+        // validated once, before any entry changes (a failure part-way through a multi-device
+        // context's entries must not leave them dealing differently)
+        uint32_t T = 0;
+        std::vector<uint32_t> pos;
+        if (order) {
+            if (width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
+                return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad resolution");
+            T = ((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
+            pos.assign(T, 0xFFFFFFFFu);
+            for (uint32_t s = 0; s < T; ++s) {
+                if (order[s] >= T || pos[order[s]] != 0xFFFFFFFFu)
+                    return fail(ctx, OCTPT_ERR_INVALID_ARG, "tile order is not a permutation of the frame's tiles");
+                pos[order[s]] = s;
+            }
+        }
+        for (size_t i = 0; i < ctx->sub.size(); ++i) {  // every device entry deals the same way (its sub-shards nest in it)
+            const octpt_status st = octpt_set_tile_order(ctx->sub[i], width, height, order);
+            if (st != OCTPT_OK) {
+                // an entry failed (out of memory): every entry and the parent go back to round robin, so that the
+                // parent's staging and the entries' item mappings agree
+                const std::string why = ctx->sub[i]->err;
+                for (octpt_ctx *c : ctx->sub) (void)octpt_set_tile_order(c, width, height, nullptr);
+                ++ctx->order_gen;
+                ctx->h_order.clear();
+                ctx->order_w = ctx->order_h = 0;
+                return fail(ctx, st, why + " (every entry reset to the round-robin deal)");
+            }
         }
         HIP_TRY(ctx, hipSetDevice(ctx->device));
         ++ctx->order_gen;
@@ -1930,16 +1994,9 @@ octpt_status octpt_set_tile_order(octpt_ctx *ctx, uint32_t width, uint32_t heigh
             ctx->order_w = ctx->order_h = 0;
             return OCTPT_OK;
         }
-        if (width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
-            return fail(ctx, OCTPT_ERR_INVALID_ARG, "bad resolution");
-        const uint32_t T = ((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
-        std::vector<uint32_t> pos(T, 0xFFFFFFFFu);
-        for (uint32_t s = 0; s < T; ++s) {
-            if (order[s] >= T || pos[order[s]] != 0xFFFFFFFFu)
-                return fail(ctx, OCTPT_ERR_INVALID_ARG, "tile order is not a permutation of the frame's tiles");
-            pos[order[s]] = s;
-        }
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // an earlier render may still read the tables
+        // the tables are overwritten in place: a render issued on any stream (render_device / unshard_device take
+        // the caller's) may still read them, so the whole device drains first
+        HIP_TRY(ctx, hipDeviceSynchronize());
         if (ctx->h_order.size() != T) {
             if (ctx->d_order) (void)hipFree(ctx->d_order);
             if (ctx->d_order_pos) (void)hipFree(ctx->d_order_pos);
@@ -2011,10 +2068,13 @@ octpt_status octpt_intersect(octpt_ctx *ctx, const float *rays, const uint32_t *
     }
     // esvo_begin's t_coef = 1 / -|d| comes from rcp_rn, exact for |d| in [2^-23, 2^126] (smaller
     // components are clamped to 2^-23 first, octree_traversal.rs:86-93): a ray with a non-finite
-    // component or a direction component |d| > 2^126 is outside that range.  The reference's Scene::hit
-    // takes any ray and reports such one as a miss (its comparisons with NaN t-values all fail), so it is
-    // reported as a miss here too -- t = +inf, prim = none, normal 0, 0 steps -- and the rest of the
-    // batch is traced as usual (the kernel sees a placeholder ray in its place).
+    // component or a direction component |d| > 2^126 is outside that range.  Such a ray is reported as a
+    // miss -- t = +inf, prim = none, normal 0, 0 steps -- and the rest of the batch is traced as usual (the
+    // kernel sees a placeholder ray in its place).  For a non-finite ray this is what the reference's
+    // comparisons with NaN t-values give.  For a finite direction above 2^126 it is a DELIBERATE DEVIATION:
+    // the reference does not normalise directions (Ray::new, ray/mod.rs:32), its t_coef would be subnormal
+    // (octree_traversal.rs:95) and its walk could still hit something; no reference fixture covers that
+    // case (parity unpinned), and the render kernels never produce such a direction.
     std::vector<uint32_t> unsupported;
     std::vector<float> clean;
     for (size_t i = 0; i < (size_t)n * 6; ++i) {

@@ -30,6 +30,11 @@ constexpr uint32_t kBeamTile = OCTPT_BEAM_TILE;
 #define OCTPT_CAM_RECORDS 1
 #endif
 #endif
+// stackless ESVO in wf_extend_kernel (north_star's "stackless octree DDA"): a pop reads the
+// ancestor from DevScene::anc instead of the LDS stack and recomputes its t_max in closed form (A/B knob)
+#ifndef OCTPT_STACKLESS
+#define OCTPT_STACKLESS 0
+#endif
 constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primary rays
 constexpr uint32_t kBlock = 256;       // threads per block (4 waves)
 constexpr uint32_t kMaxDepth = 21;     // new_octree.rs:14
@@ -100,6 +105,10 @@ struct DevScene {
     const uint2 *node_child;
     const float4 *leaf_sph;         // parallel to node_child: the sphere of a single-sphere leaf slot
     uint32_t root, root_mask, depth, n_octants;  // root = the root octant's base
+    // OCTPT_STACKLESS builds: the ancestors of every octant, row = its base (a node_child index), depth - 1
+    // entries per row; entry j = (base, mask) of the ancestor whose children are cells of level j + 1 (the
+    // LDS stack's slot j), written for the levels above the octant (build_ancestors_gpu)
+    const uint2 *anc;
     uint32_t has_cuboids;
     float octree_scale;             // 2^-depth
     float inv_octree_scale;         // 2^depth (x / 2^-depth == x * 2^depth exactly)
@@ -192,7 +201,10 @@ struct WaveBuffers {
     uint2 *pc;      // (cur_mat, depth | specular << 8 | path_segs << 16)
     uint32_t *item0;  // per slot: the chunk item the seed started there (the first shade rebuilds pa / pb / pc)
     uint2 *hit;     // per queue position: (cuboid bit | flags << 27 | prim index, t) -- hit_record()
-    float2 *huv;    // per queue position, block-value scenes only (C23): the hit's (u, v), or a quad's barycentrics
+    // per queue position, block-value scenes only (C23): the whole hit record, (face << 27 | block or the quad, t, u, v)
+    // -- the hit's texture coordinates or a quad's barycentrics beside it -- one 16-B store in extend and one
+    // 16-B load in shade (round 6; until then an 8-B `hit` record and an 8-B (u, v) record in two arrays)
+    uint4 *hit4;
     float4 *color;  // per chunk item: (L.xyz, path segments)
     // sun-sampling state, 4 planes of `pool` float4:
     // (co.xyz, clast), (cd.xyz, ccur), (cn.xyz, mult), att
@@ -300,6 +312,9 @@ hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const ui
 hipError_t launch_multi_stage(const DevRender &R, uint32_t n_dev, uint32_t stride, float4 *accum, uint32_t *seg,
                               float4 *stage_accum, uint32_t *stage_seg, bool to_stage, hipStream_t stream);
 int render_blocks_per_cu(uint32_t depth);
+// OCTPT_STACKLESS: fill anc ((depth - 1) x (n_slots + 8) uint2) from S.node_child, one launch per level from the
+// root down; f0 / f1: frontier scratch of n_octants uint2 each, d_n: 1 uint32 (all device memory)
+hipError_t build_ancestors_gpu(const DevScene &S, uint2 *anc, uint2 *f0, uint2 *f1, uint32_t *d_n, hipStream_t stream);
 size_t render_lds_bytes(uint32_t depth);
 
 // std::vector allocator that leaves resized elements uninitialised: the builders overwrite every

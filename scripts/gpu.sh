@@ -12,7 +12,7 @@
 #                         (LIB = build_variants/NAME/liboctpt.so runs that build -> stats_CFG_NAME/)
 #   pmc:CFG[:N]           FETCH_SIZE / WRITE_SIZE / TCC passes: the one-step bench (N = 1) or rank 0's shard of
 #                         an N-way split (scripts/shard_step.py) -> pmc_CFG[_nN].json, also into profiles/
-#   sq:CFG                the SQ counter pass of the one-step bench                 -> sq_CFG/
+#   sq:CFG[:LIB]          the SQ counter pass of the one-step bench (of that build)  -> sq_CFG[_NAME]/
 #   shard:CFG[:NS]        scripts/shard_emulation.py (NS = "1_2_4_8", the default)  -> shard_CFG.json
 #   n8                    bench.py --gpus 8 --dist-backend gloo (the driver's N = 8 command on one GPU)
 #   nrank:N[:CFG[:STEPS]] the same at N ranks with the CPU baseline, wall time recorded -> nrank_N_CFG.json/.time
@@ -63,11 +63,13 @@ for task in "$@"; do
       python3 scripts/pmc_traffic.py $P/fetch $P/write $a $O/pmc_$a$SUF.json 1.0 "calibrated by tools/fetch_calib.hip (profiles/fetch_calib.json): scattered 8-B and 16-B reads are counted at 64 B per request, factor 1" $P/tcc "$SRC" || fail "$task summary"
       cp $O/pmc_$a$SUF.json profiles/pmc_$a$SUF.json
       cat $P.fetch.out | tail -1 ;;
-    sq)
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
-          SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS -d $O/sq_$a -o run \
+    sq)  # sq:CFG[:LIB]  (LIB = build_variants/NAME/liboctpt.so -> sq_CFG_NAME/)
+      V=$a; if [ -n "$b" ]; then V=${a}_$(basename $(dirname $b)); fi
+      (cd /tmp && export TMPDIR=/tmp && if [ -n "$b" ]; then export OCTPT_LIB=$R/$b; fi \
+          && timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+          SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS -d $O/sq_$V -o run \
           --output-format csv -- python3 $R/bench.py --config $a --steps 1 --warmup 0 --no-cpu-baseline --no-issued \
-          > $O/sq_$a.out 2> $O/sq_$a.err) || fail "$task" $O/sq_$a.err ;;
+          > $O/sq_$V.out 2> $O/sq_$V.err) || fail "$task" $O/sq_$V.err ;;
     shard)
       NS=${b:-1_2_4_8}
       timeout -k 10 600 python3 scripts/shard_emulation.py --config $a --ns ${NS//_/ } > $O/shard_$a.json \

@@ -149,7 +149,7 @@ def test_oracle_block_hits_match_voxel_dda(compact):
     assert agree > 100
 
 
-def _reference_scene(sc: S.Scene, masks, children, depth, image: bool = True):
+def _reference_scene(sc: S.Scene, masks, children, depth, image: bool = True, root: int = 0):
     """An octpt_reference_scene holding `sc`'s materials as the reference's Material + Texture."""
     keep = []
     mats = (_lib.ReferenceMaterial * len(sc.materials))()
@@ -170,7 +170,7 @@ def _reference_scene(sc: S.Scene, masks, children, depth, image: bool = True):
     buf["m"], buf["c"] = masks, children
     blocks = sc.block_structs()
     ref = _lib.ReferenceScene()
-    ref.octants, ref.octant_count, ref.root, ref.depth = C.cast(octs, C.c_void_p), len(masks), 0, depth
+    ref.octants, ref.octant_count, ref.root, ref.depth = C.cast(octs, C.c_void_p), len(masks), root, depth
     ref.blocks, ref.block_count = C.cast(blocks, C.c_void_p), len(sc.blocks)
     ref.materials, ref.material_count = C.cast(mats, C.c_void_p), len(sc.materials)
     ref.sun = sc.sun_struct()

@@ -178,8 +178,10 @@ def test_intersect_parity(renderer):
 
 
 def test_intersect_unsupported_rays_are_misses(renderer):
-    """A ray with a non-finite component or a direction component above 2^126 is a miss (the
-    reference's Scene::hit takes any ray), and the batch's other rays are traced exactly as without it."""
+    """A ray with a non-finite component or a direction component above 2^126 is a miss, and the batch's other
+    rays are traced exactly as without it.  Non-finite rays miss in the reference too; a finite component above
+    2^126 missing is a deliberate deviation (the reference would walk on a subnormal t_coef,
+    octree_traversal.rs:95, and might hit): parity unpinned, no reference fixture covers it."""
     from octree_pathtracing_amd import scene as S
     from oracle import cpu_ref
 
