@@ -280,36 +280,12 @@ hipError_t upload(octpt_ctx *ctx, const T *src, size_t n, T **dst) {
         e = hipMemset(p, 0, bytes);
         if (e != hipSuccess) return e;
         // hipMemset runs on the null stream, which does not order itself with the context's non-blocking stream:
-        // the kernels that fill these tables on ctx->stream (fill_scene_gpu, build_ancestors_gpu) must not race it
+        // the kernels that fill these tables on ctx->stream (fill_scene_gpu) must not race it
         e = hipStreamSynchronize(nullptr);
         if (e != hipSuccess) return e;
     }
     *dst = static_cast<T *>(p);
     return hipSuccess;
-}
-
-// OCTPT_STACKLESS builds: the ancestor table the stackless pop reads (DevScene::anc, build_ancestors_gpu), one
-// row of depth - 1 entries per node_child index; a scene-lifetime allocation like the other tables
-octpt_status build_ancestor_table(octpt_ctx *ctx, DevScene &S, size_t n_slots) {
-    S.anc = nullptr;
-    if (!OCTPT_STACKLESS) return OCTPT_OK;
-    const size_t row = S.depth > 1u ? S.depth - 1u : 1u;
-    if ((n_slots + 8) * row >= (1ull << 29))  // the kernel forms 32-bit byte offsets into the table
-        return fail(ctx, OCTPT_ERR_UNSUPPORTED, "octree too large for the stackless build's ancestor table");
-    uint2 *anc = nullptr;
-    HIP_TRY(ctx, upload<uint2>(ctx, nullptr, std::max<size_t>((n_slots + 8) * row, 8), &anc));  // zeroed
-    uint2 *f = nullptr;
-    uint32_t *d_n = nullptr;
-    const size_t nf = std::max<uint32_t>(S.n_octants, 1u);
-    HIP_TRY(ctx, hipMalloc(&f, 2 * nf * sizeof(uint2)));
-    hipError_t e = hipMalloc(&d_n, sizeof(uint32_t));
-    if (e == hipSuccess) e = build_ancestors_gpu(S, anc, f, f + nf, d_n, ctx->stream);
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(f);
-    if (d_n) (void)hipFree(d_n);
-    if (e != hipSuccess) return hip_fail(ctx, e, "ancestor table");
-    S.anc = anc;
-    return OCTPT_OK;
 }
 
 // memoised subtree height with cycle detection; returns -1 on a cycle or bad index.
@@ -1663,8 +1639,6 @@ octpt_status octpt_scene_upload(octpt_ctx *ctx, const octpt_scene_desc *d) {
         S.n_octants = d->octant_count;
         st = upload_tables(ctx, d, true, S);
         if (st != OCTPT_OK) return st;
-        st = build_ancestor_table(ctx, S, n_slots);
-        if (st != OCTPT_OK) return st;
         ctx->S = S;
         ctx->has_scene = true;
         ++ctx->scene_gen;
@@ -1741,8 +1715,6 @@ octpt_status octpt_scene_build_device(octpt_ctx *ctx, const octpt_scene_desc *d,
         S.root_mask = root_mask;
         S.n_octants = t.n_octants;
         st = upload_tables(ctx, d, false, S);
-        if (st != OCTPT_OK) return st;
-        st = build_ancestor_table(ctx, S, n_slots);
         if (st != OCTPT_OK) return st;
         ctx->S = S;
         ctx->has_scene = true;

@@ -30,11 +30,6 @@ constexpr uint32_t kBeamTile = OCTPT_BEAM_TILE;
 #define OCTPT_CAM_RECORDS 1
 #endif
 #endif
-// stackless ESVO in wf_extend_kernel (north_star's "stackless octree DDA"): a pop reads the
-// ancestor from DevScene::anc instead of the LDS stack and recomputes its t_max in closed form (A/B knob)
-#ifndef OCTPT_STACKLESS
-#define OCTPT_STACKLESS 0
-#endif
 constexpr uint32_t kTile = 8;          // 8x8 pixel tiles = one wave64 of primary rays
 constexpr uint32_t kBlock = 256;       // threads per block (4 waves)
 constexpr uint32_t kMaxDepth = 21;     // new_octree.rs:14
@@ -105,10 +100,6 @@ struct DevScene {
     const uint2 *node_child;
     const float4 *leaf_sph;         // parallel to node_child: the sphere of a single-sphere leaf slot
     uint32_t root, root_mask, depth, n_octants;  // root = the root octant's base
-    // OCTPT_STACKLESS builds: the ancestors of every octant, row = its base (a node_child index), depth - 1
-    // entries per row; entry j = (base, mask) of the ancestor whose children are cells of level j + 1 (the
-    // LDS stack's slot j), written for the levels above the octant (build_ancestors_gpu)
-    const uint2 *anc;
     uint32_t has_cuboids;
     float octree_scale;             // 2^-depth
     float inv_octree_scale;         // 2^depth (x / 2^-depth == x * 2^depth exactly)
@@ -312,9 +303,6 @@ hipError_t launch_unshard(uint32_t W, uint32_t H, uint32_t shard_count, const ui
 hipError_t launch_multi_stage(const DevRender &R, uint32_t n_dev, uint32_t stride, float4 *accum, uint32_t *seg,
                               float4 *stage_accum, uint32_t *stage_seg, bool to_stage, hipStream_t stream);
 int render_blocks_per_cu(uint32_t depth);
-// OCTPT_STACKLESS: fill anc ((depth - 1) x (n_slots + 8) uint2) from S.node_child, one launch per level from the
-// root down; f0 / f1: frontier scratch of n_octants uint2 each, d_n: 1 uint32 (all device memory)
-hipError_t build_ancestors_gpu(const DevScene &S, uint2 *anc, uint2 *f0, uint2 *f1, uint32_t *d_n, hipStream_t stream);
 size_t render_lds_bytes(uint32_t depth);
 
 // std::vector allocator that leaves resized elements uninitialised: the builders overwrite every

@@ -15,8 +15,6 @@
 // reference's operation order.  The only difference is the radiance accumulation order
 // (forward throughput instead of the reference's recursion), which the oracle also
 // implements as `forward_accumulation`.
-#include <type_traits>
-
 #include "octpt_internal.h"
 #include "octpt_rcp.h"
 
@@ -206,44 +204,24 @@ struct TraceRay {
 // per-lane ESVO stack in LDS: entry (parent base, t_max) and 16-bit mask per scale, lanes
 // interleaved with stride kStride (the threads of the block that traverse).  (A packed 9-B entry for a
 // seventh wave of the depth-11 instances lost, round 5: tools/rejected/packed_stack.patch.)
-// OCTPT_STACK_TMAX=0 (A/B knob): 6-B entries without t_max, which a pop recomputes in closed form instead (the exit
-// t of the popped octant's cell, esvo_step's pop): 15 KB instead of 25.6 KB per depth-11 block
-#ifndef OCTPT_STACK_TMAX
-#define OCTPT_STACK_TMAX 1
-#endif
+// (Measured and rejected, round 6: the stackless traversal -- ancestors from a per-octant table, t_max in closed
+// form -- and entries without t_max, tools/rejected/stackless.patch)
 template <uint32_t kStride>
 struct StackT {
-#if OCTPT_STACK_TMAX
     uint2 *e;
-#else
-    uint32_t *e;
-#endif
     uint16_t *m;
     __device__ __forceinline__ void write(uint32_t slot, uint32_t node, float t, uint32_t mask) const {
-#if OCTPT_STACK_TMAX
         e[slot * kStride] = make_uint2(node, __float_as_uint(t));
-#else
-        e[slot * kStride] = node;
-#endif
         m[slot * kStride] = (uint16_t)mask;
     }
     __device__ __forceinline__ void read(uint32_t slot, uint32_t &node, float &t, uint32_t &mask) const {
-#if OCTPT_STACK_TMAX
         const uint2 v = e[slot * kStride];
         node = v.x;
-        t = __uint_as_float(v.y);
-#else
-        node = e[slot * kStride];
-#endif
         mask = m[slot * kStride];
+        t = __uint_as_float(v.y);
     }
 };
 using Stack = StackT<kBlock>;
-// the stackless traversal (OCTPT_STACKLESS): no per-lane stack at all; a pop reads the ancestor
-// from the scene's ancestor table (DevScene::anc) and recomputes its t_max from the truncated position
-struct NoStack {};
-template <class Stk>
-constexpr bool kIsStackless = std::is_same<Stk, NoStack>::value;
 
 // Path state between segments (Ray + HitRecord of ray/mod.rs:16-23, hittable/mod.rs:53-84,
 // plus the forward throughput T / radiance L of the kernel's accumulation order).
@@ -833,18 +811,12 @@ template <uint32_t kS>
 __device__ __forceinline__ void stk_write(const StackT<kS> &stk, uint32_t slot, uint32_t node, float t, uint32_t mask) {
     stk.write(slot, node, t, mask);
 }
-__device__ __forceinline__ void stk_write(const NoStack &, uint32_t, uint32_t, float, uint32_t) {}
 
 template <uint32_t kS = kBlock>
 __device__ __forceinline__ StackT<kS> stack_of(uint2 *lds, uint32_t depth) {
     StackT<kS> s;
-#if OCTPT_STACK_TMAX
     s.e = lds + threadIdx.x;
     s.m = reinterpret_cast<uint16_t *>(lds + (size_t)(depth - 1u) * kS) + threadIdx.x;
-#else
-    s.e = reinterpret_cast<uint32_t *>(lds) + threadIdx.x;
-    s.m = reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(lds) + (size_t)(depth - 1u) * kS) + threadIdx.x;
-#endif
     return s;
 }
 
@@ -891,8 +863,8 @@ __device__ __forceinline__ void esvo_root(const DevScene &S, Esvo &E) {
 // hold a bound of the reference iterations before the start (beam_kernel), at which the iteration
 // count begins, so that the reference's step cap still applies (a ray reaching it is traced again from
 // its cube entry, esvo_capped).
-template <class Stk>
-__device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const Stk &stk,
+template <uint32_t kS>
+__device__ inline void esvo_begin(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk,
                                   float t_start = 0.0f) {
     const float osc = S.octree_scale;
     // The reference zero-initialises the stack (octree_traversal.rs:69-70).  ESVO only pops to a
@@ -936,8 +908,8 @@ enum : int { kStepContinue = 0, kStepHit = 1, kStepMiss = 2 };
 // One descend-only ESVO iteration (octree_traversal.rs:216-244, counted in E.iter) into the child
 // whose slot is (its base, its mask); tc / tc_max / tv_max are the current cell's t_corner, its
 // minimum and min(t_max, tc_max).  The same operations as esvo_step's descend.
-template <class Stk>
-__device__ __forceinline__ void esvo_descend(Esvo &E, const Stk &stk, uint32_t depth, v3 tc, float tc_max,
+template <uint32_t kS>
+__device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uint32_t depth, v3 tc, float tc_max,
                                              float tv_max, uint2 slot) {
     E.iter += 1u;
     const float half = E.scale_exp2 * 0.5f;
@@ -947,10 +919,8 @@ __device__ __forceinline__ void esvo_descend(Esvo &E, const Stk &stk, uint32_t d
     if (dy) E.pos.y = E.pos.y + half;
     if (dz) E.pos.z = E.pos.z + half;
     const uint32_t slot_u = (__float_as_uint(E.scale_exp2) >> 23) - 128u + depth;
-    if constexpr (!kIsStackless<Stk>) {
-        if (tc_max < E.h) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
-        E.h = tc_max;
-    }
+    if (tc_max < E.h) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
+    E.h = tc_max;
     E.parent = slot.x;
     E.pmask = slot.y;
     E.scale_exp2 = half;
@@ -1083,8 +1053,8 @@ __device__ inline bool leaf_test(const DevScene &S, const TraceRay &r, const Esv
 // primitive hit.  The step-limit / max_dst miss is taken at the end: a lane past either runs the
 // step with no memory side effects (not live) and reports the miss, so the exit costs no exec-mask
 // region.  Callers add E.iter to cnt.steps when the ray finishes.
-template <int kPrims = kPrimsModels, bool kFast = false, class Stk = Stack>
-__device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const Stk &stk, Counters &cnt,
+template <int kPrims = kPrimsModels, bool kFast = false, uint32_t kS = kBlock>
+__device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E, const StackT<kS> &stk, Counters &cnt,
                                 uint32_t &prim, PrimHit &h) {
     // :128-130: max_dst = 1024 * 2^-depth > 0, so the reference's `max_dst >= 0` guard always holds
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
@@ -1159,10 +1129,8 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // 1..depth-1 (stack slot = level - 1 >= 0; the oracle's level-0 entry stays zero, like the miss
     // below).  One guarded write, so that the selects below stay branch-free.
     const uint32_t slot_u = (__float_as_uint(E.scale_exp2) >> 23) - 128u + S.depth;
-    if constexpr (!kIsStackless<Stk>) {  // (the stackless traversal keeps no stack and no h)
-        if (descend & (tc_max < E.h)) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
-        E.h = descend ? tc_max : E.h;
-    }
+    if (descend & (tc_max < E.h)) stk_write(stk, slot_u, E.parent, E.t_max, E.pmask);
+    E.h = descend ? tc_max : E.h;
 #ifdef OCTPT_SLOT_LEAK_PROBE
     // negative control of SLOT_CHECK (scripts/stale_hit_probe.py slotleak_check): a lane advancing past an
     // absent child takes the slot it never loaded; the check build must count it
@@ -1255,37 +1223,12 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         // mantissa, always differs, and the pop condition means a higher one does), so
         // scale > base = OCTREE_MAX_SCALE - depth and the entry is in the LDS stack (levels 1..)
         const uint32_t base1 = OCTREE_MAX_SCALE + 1u - S.depth;  // base + 1, wave-uniform
-        uint2 anc;
-        if constexpr (kIsStackless<Stk>) {
-            // the ancestor whose children have this scale: entry scale - base1 of the current octant's row (the
-            // octant's base is its row), one load in place of the LDS stack's read
-            // (an escaping lane loads row 0's first entry instead: its clamped scale may lie outside any row)
-            // (a 32-bit byte offset from the table's base: the upload keeps the table below 2^29 entries)
-            const uint32_t off = esc ? 0u : (E.parent * (S.depth - 1u) + (scale - base1)) * 8u;
-            anc = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(S.anc) + off);
-            ISSUED(cnt, 8);
-        } else {
-            stk.read(scale - base1, E.parent, E.t_max, E.pmask);
-        }
+        stk.read(scale - base1, E.parent, E.t_max, E.pmask);
         // pos truncated to the popped scale; idx = pos bits at that scale
         const uint32_t keep = 0xFFFFFFFFu << scale;
         const uint32_t px = __float_as_uint(E.pos.x) & keep, py = __float_as_uint(E.pos.y) & keep,
                        pz = __float_as_uint(E.pos.z) & keep;
         E.pos = V(__uint_as_float(px), __uint_as_float(py), __uint_as_float(pz));
-        if constexpr (kIsStackless<Stk> || !OCTPT_STACK_TMAX) {
-            // The ancestor's t_max in closed form: the exit t of its own cell (corner = pos truncated one level
-            // higher).  The stack held min(root t_max, the exit t of every enclosing cell) (descend: t_max =
-            // min(t_max, tc_max)), and for nested cells the corner moves monotonically (a child's corner is >= its
-            // parent's per axis, t_coef < 0), and so does each rounded pos * t_coef - t_bias: the innermost cell's
-            // exit is that minimum bit for bit; the root's cell (corner 1) gives esvo_root's t_max itself.
-            const uint32_t keep2 = keep << 1;
-            const v3 corner = V(__uint_as_float(px & keep2), __uint_as_float(py & keep2), __uint_as_float(pz & keep2));
-            E.t_max = tmin3(vsub(vmul(corner, E.t_coef), E.t_bias));
-            if constexpr (kIsStackless<Stk>) {
-                E.parent = anc.x;
-                E.pmask = anc.y;
-            }
-        }
         E.idx = __builtin_amdgcn_ubfe(px, scale, 1u) | (__builtin_amdgcn_ubfe(py, scale, 1u) << 1) |
                 (__builtin_amdgcn_ubfe(pz, scale, 1u) << 2);
         // h = 0 after a pop (:298); an escaped lane's h = -1 carries the escape out of the branch, where
@@ -2221,12 +2164,8 @@ constexpr uint32_t kShortRaySteps = OCTPT_SHORT_STEPS;
 template <int kPrims>
 __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_extend_kernel(DevScene S, WaveBuffers B, uint32_t q, uint32_t refill,
                                                            unsigned long long *__restrict__ stats) {
-#if OCTPT_STACKLESS
-    const NoStack stk{};  // no LDS (launch_wf_extend passes 0 bytes)
-#else
     extern __shared__ uint2 lds_stack[];
     const Stack stk = stack_of(lds_stack, S.depth);
-#endif
     const float4 *ray0 = B.ray0[q], *ray1 = B.ray1[q];
     // refill bit 31 (launch_wf_extend's cam): the queue holds the seed's 16-B camera records (store_cam_ray), whose
     // origin record (eye, kPrimNone) the seed left at ray0[0] (no LDS for it: one more LDS granule per block
@@ -3024,9 +2963,7 @@ __global__ void multi_stage_kernel(DevRender R, uint32_t n_dev, uint32_t stride,
 }  // namespace
 
 // ESVO stack levels 1..depth-1 (level 0 is never used, see esvo_step)
-size_t render_lds_bytes(uint32_t depth) {
-    return (size_t)(depth - 1u) * kBlock * ((OCTPT_STACK_TMAX ? sizeof(uint2) : sizeof(uint32_t)) + sizeof(uint16_t));
-}
+size_t render_lds_bytes(uint32_t depth) { return (size_t)(depth - 1u) * kBlock * (sizeof(uint2) + sizeof(uint16_t)); }
 
 int render_blocks_per_cu(uint32_t depth) {
     int blocks = 0;
@@ -3044,12 +2981,9 @@ static const void *extend_instance(const DevScene &S) {
     return reinterpret_cast<const void *>(wf_extend_kernel<kPrimsSpheres>);
 }
 
-// dynamic LDS of wf_extend_kernel: the ESVO stack, none in the stackless build
-static size_t extend_lds_bytes(uint32_t depth) { return OCTPT_STACKLESS ? 0u : render_lds_bytes(depth); }
-
 int extend_blocks_per_cu(const DevScene &S) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S), kBlock, extend_lds_bytes(S.depth)) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, extend_instance(S), kBlock, render_lds_bytes(S.depth)) !=
         hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
@@ -3099,7 +3033,7 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
     // refill 0: the adaptive threshold; cam: queue q holds the seed's camera records (refill bit 31)
     uint32_t rf = refill | (cam ? 0x80000000u : 0u);
     void *args[] = {const_cast<DevScene *>(&S), const_cast<WaveBuffers *>(&B), &q, &rf, &stats};
-    const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, extend_lds_bytes(S.depth),
+    const hipError_t e = hipLaunchKernel(extend_instance(S), dim3(grid), dim3(kBlock), args, render_lds_bytes(S.depth),
                                          stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
@@ -3197,47 +3131,6 @@ hipError_t launch_beam(const DevScene &S, const DevCamera &C, const DevRender &R
 #endif
     hipLaunchKernelGGL(beam_kernel, dim3((n + per_block - 1u) / per_block), dim3(64), lds, stream, S, C, R, n, beam);
     return hipGetLastError();
-}
-
-// One level of the ancestor table (OCTPT_STACKLESS): every octant of the frontier (cur: (base, mask), children
-// of cell level lvl) writes the row of each octant child: entry lvl - 1 = itself, entries >= lvl = its own row's
-// (its ancestors), and appends the child to the next frontier.
-__global__ __launch_bounds__(256) void anc_level_kernel(DevScene S, const uint2 *__restrict__ cur, uint32_t n_cur,
-                                                        uint32_t lvl, uint2 *__restrict__ anc, uint2 *__restrict__ next,
-                                                        uint32_t *__restrict__ n_next) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_cur) return;
-    const uint2 o = cur[i];
-    const uint32_t row = S.depth - 1u;
-    uint32_t k = o.x;
-    for (uint32_t c = 0; c < 8u; ++c) {
-        if (!((o.y >> c) & 1u)) continue;
-        const uint2 ch = S.node_child[k++];
-        if ((o.y >> (c + 8u)) & 1u) continue;  // a leaf
-        uint2 *dst = anc + (size_t)ch.x * row;
-        const uint2 *src = anc + (size_t)o.x * row;
-        dst[lvl - 1u] = o;
-        for (uint32_t j = lvl; j < row; ++j) dst[j] = src[j];
-        next[atomicAdd(n_next, 1u)] = ch;
-    }
-}
-
-hipError_t build_ancestors_gpu(const DevScene &S, uint2 *anc, uint2 *f0, uint2 *f1, uint32_t *d_n, hipStream_t stream) {
-    if (S.depth < 2u || S.n_octants == 0u || (S.root_mask & 0xFFu) == 0u) return hipSuccess;
-    const uint2 root = make_uint2(S.root, S.root_mask);
-    hipError_t e = hipMemcpyAsync(f0, &root, sizeof root, hipMemcpyHostToDevice, stream);
-    if (e != hipSuccess) return e;
-    uint32_t n = 1u;
-    for (uint32_t lvl = S.depth - 1u; lvl >= 1u && n > 0u; --lvl) {  // the root's children are cells of level depth - 1
-        if ((e = hipMemsetAsync(d_n, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        hipLaunchKernelGGL(anc_level_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, S, f0, n, lvl, anc, f1, d_n);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if ((e = hipMemcpyAsync(&n, d_n, sizeof n, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
-        if (n > S.n_octants) return hipErrorInvalidValue;  // (a malformed tree; upload validates it)
-        std::swap(f0, f1);
-    }
-    return hipSuccess;
 }
 
 hipError_t launch_tonemap(const float4 *accum, uchar4 *out, uint32_t n, const uint8_t *lut_byte, hipStream_t stream) {
