@@ -274,41 +274,29 @@ def capi_devices(spec: str, n_visible: int) -> list:
     return [i % max(n_visible, 1) for i in range(int(spec))]
 
 
-def capi_multi_measure(sc, cam, rs, devices, steps: int, warmup: int) -> dict:
-    """The multi-device path a Rust host calls (octpt_create_multi): one process, one context
-    over `devices`, whole frames through octpt_render_device into a frame buffer on devices[0] (tiles dealt
-    over the entries, gathered with peer copies inside liboctpt).  Whole-job Mrays/s over the timed steps."""
-    import torch
-    from octree_pathtracing_amd.renderer import HipRenderer
+def capi_multi_measure(config: str, devices, steps: int, warmup: int, spp=None, compact: bool = False,
+                       timeout: float = 600.0) -> dict:
+    """The multi-device path a Rust host calls (octpt_create_multi): one process, one context over
+    `devices`, whole frames through octpt_render_device into a frame buffer on devices[0] (tiles dealt over the
+    entries, gathered with peer copies inside liboctpt) -- `bench.py --capi-devices` run as a child process, so that
+    a failure of this extra leg (the first distinct-device peer copies on a node) is reported in the line instead
+    of ending the N-rank bench that runs it.  Whole-job Mrays/s over the timed steps."""
+    import subprocess
 
-    W, H = rs.width, rs.height
-    r = HipRenderer(devices=devices)
-    try:
-        r.set_scene(sc)
-        r.set_camera(cam)
-        r.max_depth, r.seed = rs.max_depth, rs.seed
-        dev = torch.device("cuda", devices[0])
-        acc = torch.zeros((W * H, 4), dtype=torch.float32, device=dev)
-        p = r.params(W, H, 0, rs.spp)
-        with torch.cuda.device(dev):
-            stream = torch.cuda.current_stream().cuda_stream
-            for _ in range(warmup):
-                acc[:, 3] = 1.0
-                r.render_device(p, acc.data_ptr(), None, stream)
-            torch.cuda.synchronize()
-            r.reset_stats()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                r.set_camera(cam)  # the beam tables recomputed every step, as in the main loop
-                r.render_device(p, acc.data_ptr(), None, stream)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-        st = r.stats()
-    finally:
-        r.close()
-    return {"value": round(st["segments"] / dt / 1e6, 2), "unit": "Mrays/s", "devices": list(devices),
-            "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "segments": st["segments"],
-            "path": "octpt_create_multi + octpt_render_device (one process, peer-copy gather inside liboctpt)"}
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--config", config, "--capi-devices",
+           ",".join(str(d) for d in devices), "--steps", str(steps), "--warmup", str(warmup), "--no-cpu-baseline",
+           "--no-issued", *(["--spp", str(spp)] if spp else []), *(["--compact"] if compact else [])]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit {p.returncode}: {(p.stderr or p.stdout)[-600:]}", "devices": list(devices)}
+    d = json.loads(lines[-1])
+    return {"value": d["value"], "unit": d["unit"], "devices": d["config"]["capi_devices"],
+            "ms_per_step": d["ms_per_step"], "steps": d["steps"], "segments": d["config"]["segments_per_step"],
+            "path": "octpt_create_multi + octpt_render_device (one child process, peer-copy gather inside liboctpt)"}
 
 
 def balance_deal(r, segbuf, n_local: int, W: int, H: int, rank: int, world: int, cdev, balance_tiles) -> str:
@@ -576,7 +564,8 @@ def main():
         if rank == 0:
             try:
                 devs = [i % max(n_dev, 1) for i in range(world)]
-                out["capi_multi"] = capi_multi_measure(sc, cam, rs, devs, args.steps, args.warmup)
+                out["capi_multi"] = capi_multi_measure(args.config, devs, args.steps, args.warmup, args.spp,
+                                                       args.compact)
             except Exception as e:  # reported, never fatal to the bench line
                 out["capi_multi"] = {"error": f"{type(e).__name__}: {e}"}
         dist.barrier(group=host_group)
