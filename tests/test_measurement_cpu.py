@@ -129,3 +129,42 @@ def test_roofline_over_ranks():
     assert r["aggregate_gbs"] == round(7e12 / 1.5 / 1e9, 1) and r["aggregate_peak"] == 16000.0
     assert r["frac_min"] == 0.25 and r["frac_max"] == 0.5
     assert sum(x["bytes"] for x in r["per_rank"]) == 7e12 and [x["rank"] for x in r["per_rank"]] == [0, 1]
+
+
+def test_measured_rates_from_same_n_profiles():
+    """roofline.measured: the same-N profile's FETCH_SIZE / WRITE_SIZE bytes per extend launch
+    over the run's extend launch time, as GB/s and fractions of the HBM peak; every rank count the driver runs has a
+    committed profile of its own N."""
+    import json
+
+    import bench
+
+    for n in (1, 2, 4, 8):
+        assert (ROOT / "profiles" / bench.pmc_name("C3", n)).exists(), n
+        ext = json.loads((ROOT / "profiles" / bench.pmc_name("C3", n)).read_text())["wf_extend_kernel"]
+        m = bench.measured_rates("C3", n, 0.02)
+        assert m["source"] == f"profiles/{bench.pmc_name('C3', n)}"
+        assert m["read_gbs"] == round(ext["fetch_bytes_per_launch"] / 0.02 / 1e9, 1)
+        assert m["write_gbs"] == round(ext["write_bytes_per_launch"] / 0.02 / 1e9, 1)
+        assert m["read_frac"] == round(m["read_gbs"] / bench.HBM_PEAK_GBS, 4)
+    # the N-way profiles are rank 0's shard: their bytes fall with N
+    per = [json.loads((ROOT / "profiles" / bench.pmc_name("C3", n)).read_text())["wf_extend_kernel"]["bytes_per_launch"]
+           for n in (1, 2, 4, 8)]
+    assert per == sorted(per, reverse=True)
+    assert bench.measured_rates("no-such-config", 1, 0.02) is None
+    assert bench.measured_rates("C3", 3, 0.02) is None  # no profile taken at 3 ranks
+    assert bench.measured_rates("C3", 1, 0.0) is None
+
+
+def test_stdout_to_stderr_catches_native_writes():
+    """bench.stdout_to_stderr: output written to fd 1 by native code (gloo's connect messages) goes to stderr, so the
+    bench's stdout carries its one JSON line alone."""
+    import subprocess
+    import sys
+
+    code = ("import os, sys; sys.path.insert(0, %r); import bench\n"
+            "with bench.stdout_to_stderr():\n    os.write(1, b'native noise\\n')\n"
+            "print('{\"line\": 1}')\n") % str(ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout == '{"line": 1}\n' and "native noise" in p.stderr
