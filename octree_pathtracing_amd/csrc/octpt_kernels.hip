@@ -952,6 +952,10 @@ __device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uin
 #ifndef OCTPT_DFOLD_SPHERES
 #define OCTPT_DFOLD_SPHERES 1
 #endif
+// descend folds per step where the descend fold is on (A/B knob)
+#ifndef OCTPT_DFOLD_N
+#define OCTPT_DFOLD_N 1
+#endif
 // the block-value instance (C23): absent-sibling folds per step and the descend fold (A/B knobs)
 #ifndef OCTPT_FOLD_BLOCKS
 #define OCTPT_FOLD_BLOCKS 2
@@ -1151,8 +1155,12 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
     // descend-after-descend pairs (tools/esvo_trace.py).  That iteration is run here as an exact
     // replica (its own stop tests, t_corner, push and child choice, counted in E.iter); its slot
     // load depends on this step's, which the other waves of the SIMD hide.
-    if ((OCTPT_DFOLD != 3 || kPrims == kPrimsModels || (kPrims == kPrimsBlocks && OCTPT_DFOLD_BLOCKS) ||
-         (kPrims == kPrimsSpheres && OCTPT_DFOLD_SPHERES)) && descend) {
+    constexpr int kDFolds = (OCTPT_DFOLD != 3 || kPrims == kPrimsModels || (kPrims == kPrimsBlocks && OCTPT_DFOLD_BLOCKS) ||
+                             (kPrims == kPrimsSpheres && OCTPT_DFOLD_SPHERES)) ? OCTPT_DFOLD_N : 0;
+    bool dmore = descend;
+#pragma unroll
+    for (int k = 0; k < kDFolds; ++k) {  // up to kDFolds descend-only iterations after a descend (A/B: OCTPT_DFOLD_N)
+    if (dmore) {
         const uint32_t cidx2 = E.idx ^ E.mirror;
         const v3 tc2 = vsub(vmul(E.pos, E.t_coef), E.t_bias);
         const float tc2_max = tmin3(tc2);
@@ -1167,6 +1175,8 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
             ISSUED(cnt, 8);
             esvo_descend(E, stk, S.depth, tc2, tc2_max, tv2_max, slot2);
         }
+        dmore = d2;
+    }
     }
 #endif
 #if OCTPT_FOLD
