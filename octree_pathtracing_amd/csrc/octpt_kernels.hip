@@ -2160,6 +2160,10 @@ __global__ __launch_bounds__(kBlock) void wf_seed_kernel(DevCamera C, DevRender 
 #define OCTPT_CLAIM 64
 #endif
 constexpr uint32_t kClaim = OCTPT_CLAIM;
+#ifndef OCTPT_XCD_SEGS
+#define OCTPT_XCD_SEGS 0
+#endif
+static_assert(kSegs % 8u == 0u, "eight XCDs share the segments evenly");
 // refill == 0 (adaptive): rays shorter than this many ESVO steps on average refill 32 at a time
 #ifndef OCTPT_THR_LONG
 #define OCTPT_THR_LONG 16   // refill threshold of waves with long rays (A/B knob)
@@ -2187,7 +2191,15 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
         B.ctrl[ctr_head(q ^ 1u, threadIdx.x)] = 0u;
     }
     // the wave starts on its home segment (seg, seg_n rays: wave-uniform)
+#if OCTPT_XCD_SEGS
+    // XCD-aware home segments (A/B knob): blocks are dealt round robin over the 8 XCDs (block b on XCD b % 8), so
+    // XCD x takes the 8 contiguous segments 8x .. 8x + 7 -- one band of the image per XCD, whose geometry its own L2
+    // holds -- instead of the two bands 4x .. 4x + 3 and 4x + 32 .. 4x + 35 the plain modulo gives it
+    uint32_t seg = __builtin_amdgcn_readfirstlane(
+        (blockIdx.x % 8u) * (kSegs / 8u) + ((blockIdx.x / 8u) * (kBlock / 64u) + (threadIdx.x >> 6)) % (kSegs / 8u));
+#else
     uint32_t seg = __builtin_amdgcn_readfirstlane(((blockIdx.x * kBlock + threadIdx.x) >> 6) % kSegs);
+#endif
     uint32_t seg_n = B.ctrl[ctr_count(q, seg)];
     // (the block-model instance holds seg_n in an SGPR: in a VGPR it was spilled, C5 extend -1 %)
     if constexpr (kPrims == kPrimsModels) seg_n = __builtin_amdgcn_readfirstlane(seg_n);

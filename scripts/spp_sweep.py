@@ -12,6 +12,18 @@ r = HipRenderer(0)
 r.max_depth = rs.max_depth
 r.set_scene(sc); r.set_camera(cam)
 W, H = rs.width, rs.height
+if os.environ.get("TILE_ORDER") == "morton":  # experiments: dealing position -> tile in Morton (Z) order of the tile grid
+    import numpy as np
+    tx, ty = (W + 7) // 8, (H + 7) // 8
+    t = np.arange(tx * ty)
+    x, y = t % tx, t // tx
+    def part(v):
+        v = v.astype(np.uint64) & 0xFFFF
+        v = (v | (v << 8)) & 0x00FF00FF
+        v = (v | (v << 4)) & 0x0F0F0F0F
+        v = (v | (v << 2)) & 0x33333333
+        return (v | (v << 1)) & 0x55555555
+    r.set_tile_order(W, H, t[np.argsort(part(x) | (part(y) << 1), kind="stable")])
 acc = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"); acc[:, 3] = 1
 mega = "--mega" in sys.argv
 for spp in [int(x) for x in (a for a in sys.argv[2:] if not a.startswith("--"))] or [4, 16, 64, 256]:
