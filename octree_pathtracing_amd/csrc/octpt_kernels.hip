@@ -929,6 +929,28 @@ __device__ __forceinline__ void esvo_descend(Esvo &E, const StackT<kS> &stk, uin
 }
 
 
+#ifndef OCTPT_LEAD_LOOP
+#define OCTPT_LEAD_LOOP 0
+#endif
+// The descends a ray's ESVO takes before its first other iteration, as a loop of exact descend replicas
+// (esvo_descend: the same stop tests, t-values, push and child choice as esvo_step's descend), each one
+// dependent node-slot load.  A lane leaves the loop at the first iteration that would not descend.
+template <class Stk>
+__device__ __forceinline__ void lead_descends(const DevScene &S, Esvo &E, const Stk &stk) {
+    const float max_dst = MAX_DST_WORLD * S.octree_scale;
+    for (;;) {
+        const uint32_t cidx = E.idx ^ E.mirror;
+        const v3 tc = vsub(vmul(E.pos, E.t_coef), E.t_bias);
+        const float tc_max = tmin3(tc);
+        const float tv_max = tmn_nc(E.t_max, tc_max);
+        const bool d = (((E.pmask >> cidx) & 0x101u) == 0x001u) & !esvo_capped(E.iter) & !(E.t_min > max_dst) &
+                       (E.t_min <= tv_max);
+        if (!d) break;
+        const uint2 slot = S.node_child[E.parent + __popc(E.pmask & ((1u << cidx) - 1u))];
+        esvo_descend(E, stk, S.depth, tc, tc_max, tv_max, slot);
+    }
+}
+
 #ifndef OCTPT_FOLD
 #define OCTPT_FOLD 1  // absent-sibling folds per step (A/B: -DOCTPT_FOLD=0)
 #endif
@@ -2263,6 +2285,12 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
                                         (__float_as_uint(r1.w) >> 31) != 0u);
                     esvo_begin(S, tr, E, stk, bm);
                     cnt.steps -= E.iter;  // a beam start's bound of skipped iterations: executed ones are counted
+#if OCTPT_LEAD_LOOP
+                    // the ray's leading descends (octree_traversal.rs:216-244, exact replicas counted in E.iter) in a
+                    // tight loop of the refilled lanes, while the wave refills anyway, instead of one main-loop step
+                    // per level (A/B knob)
+                    lead_descends(S, E, stk);
+#endif
                 }
             }
             const uint32_t took = min((uint32_t)__popcll(im), avail);
