@@ -674,7 +674,11 @@ octpt_status make_render(octpt_ctx *ctx, const octpt_render_params *p, DevRender
     const uint32_t tiles_y = (p->height + kTile - 1) / kTile;
     R.shard_tiles = tiles_of_shard(R.tiles_x * tiles_y, p->shard_index, p->shard_count);
     R.total_items = R.shard_tiles * 64u;
+    R.div_tiles_x = udiv_magic(R.tiles_x);
+    R.div_items = udiv_magic(R.total_items);
     R.dim = (float)std::max(p->width, p->height);
+    R.jlo = -1.0f / R.dim;
+    R.jhi = 1.0f / R.dim;
     R.subs = nullptr;
     R.beam = nullptr;
     R.beam_tx = (p->width + kBeamTile - 1) / kBeamTile;

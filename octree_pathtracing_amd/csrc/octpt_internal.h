@@ -133,6 +133,20 @@ struct DevCamera {
     float d_factor;  // 1 / tan(fov / 2)  (camera.rs:79)
 };
 
+// n / d for a divisor d fixed per launch (Lemire, Kaser & Kurz 2019, "Faster remainder by direct computation"):
+// with c = ceil(2^64 / d), floor(c * n / 2^64) = floor(n / d) for every 32-bit n and 2 <= d < 2^32; c = 0 marks d = 1.
+// Two integer multiplies instead of the ~25-instruction runtime division (item -> pixel maps of seed, shade, resolve).
+inline uint64_t udiv_magic(uint32_t d) { return d <= 1u ? 0ull : ~0ull / d + 1ull; }
+__host__ __device__ inline uint32_t udiv_c(uint32_t n, uint64_t c) {
+    if (c == 0ull) return n;
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint64_t hi = (uint64_t)(uint32_t)(c >> 32) * n + __umulhi((uint32_t)c, n);
+#else
+    const uint64_t hi = (uint64_t)(uint32_t)(c >> 32) * n + (((uint64_t)(uint32_t)c * n) >> 32);
+#endif
+    return (uint32_t)(hi >> 32);
+}
+
 struct DevRender {
     uint32_t W, H;
     uint32_t spp_start, spp_count;
@@ -141,9 +155,12 @@ struct DevRender {
     uint32_t shard_index, shard_count;
     uint32_t compact;        // accum holds the shard's tiles only (tile-major)
     uint32_t tiles_x;        // ceil(W / 8)
+    uint64_t div_tiles_x, div_items;  // udiv_magic(tiles_x), udiv_magic(total_items)
     uint32_t shard_tiles;    // tiles owned by this shard
     uint32_t total_items;    // shard_tiles * 64 work items
     float dim;               // max(W, H)
+    float jlo, jhi;          // -1 / dim, 1 / dim: the jitter range of render_tile_average (tile_renderer.rs:701-702),
+                             // divided once on the host (IEEE division, the same bits as the device's)
     uint32_t preview;        // RendererMode::Preview
     // branch schedule, NULL when branch_count == 1: sub-sample k of this call is
     // subs[k] = (pass spp, pass branch count | branch << 16); spp_count then counts sub-samples

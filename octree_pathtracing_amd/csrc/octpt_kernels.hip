@@ -1435,10 +1435,10 @@ __device__ inline v3 random_sun_direction(const DevSun &K, uint32_t &rng) {
 // path logic shared by the megakernel and the wavefront shade kernel
 // ---------------------------------------------------------------------------
 // camera ray + fresh path (camera.rs:77-86, tile_renderer.rs:695-703)
-__device__ inline void new_path(const DevCamera &C, const DevRender &R, uint32_t pix, uint32_t sample, PathState &ps) {
-    const uint32_t x = pix % R.W, y = pix / R.W;
-    ps.rng = path_state(R.seed, pix, sample);
-    const float jlo = -1.0f / R.dim, jhi = 1.0f / R.dim;
+__device__ inline void new_path(const DevCamera &C, const DevRender &R, uint32_t x, uint32_t y, uint32_t sample,
+                                PathState &ps) {
+    ps.rng = path_state(R.seed, y * R.W + x, sample);
+    const float jlo = R.jlo, jhi = R.jhi;  // -1 / dim, 1 / dim (make_render)
     const float xn = ((float)(2u * x + 1u) - (float)R.W) / R.dim;
     const float yn = ((float)(2u * (R.H - y) - 1u) - (float)R.H) / R.dim;
     const float dx = jlo + (jhi - jlo) * rng_next(ps.rng);
@@ -1639,11 +1639,15 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// kFastDiv: the tile row by udiv_c (the seed, resolve and beam kernels); false: the plain division, which the shade
+// kernel's first-launch path keeps (its allocation is sensitive to that path's shape: the fast form measured shade +7 %)
+template <bool kFastDiv = true>
 __device__ __forceinline__ void item_pixel(const DevRender &R, uint32_t item, uint32_t &x, uint32_t &y) {
     const uint32_t lt = item >> 6, w = item & 63u;
     const uint32_t t = dealt_tile(R.tile_order, R.shard_index + lt * R.shard_count);
-    x = (t % R.tiles_x) * kTile + (w & 7u);
-    y = (t / R.tiles_x) * kTile + (w >> 3);
+    const uint32_t ty = kFastDiv ? udiv_c(t, R.div_tiles_x) : t / R.tiles_x;
+    x = (t - ty * R.tiles_x) * kTile + (w & 7u);
+    y = ty * kTile + (w >> 3);
 }
 
 __device__ inline unsigned long long wave_sum(uint32_t v) {
@@ -1737,7 +1741,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(DevScene S, DevCamera C,
         }
         if (__ballot(state != ST_DONE) == 0ull) break;
         if (state == ST_NEWPATH) {
-            new_path(C, R, pix, R.spp_start + k, ray);
+            new_path(C, R, pix % R.W, pix / R.W, R.spp_start + k, ray);
             cnt.paths++;
             state = ST_BEGIN;
         }
@@ -2009,10 +2013,12 @@ __device__ __forceinline__ void load_path(const WaveBuffers &B, uint32_t slot, f
 }
 
 // the path of chunk item `item`, its first segment begun; false when the pixel lies outside the image
-__device__ __forceinline__ bool item_path(const DevCamera &C, const DevRender &R, uint32_t item, PathState &ps) {
-    const uint32_t px_item = item % R.total_items, s_local = item / R.total_items;
-    uint32_t x, y;
-    item_pixel(R, px_item, x, y);
+template <bool kFastDiv = true>
+__device__ __forceinline__ bool item_path(const DevCamera &C, const DevRender &R, uint32_t item, PathState &ps,
+                                          uint32_t &x, uint32_t &y) {
+    const uint32_t s_local = kFastDiv ? udiv_c(item, R.div_items) : item / R.total_items;
+    const uint32_t px_item = item - s_local * R.total_items;
+    item_pixel<kFastDiv>(R, px_item, x, y);
     if (x >= R.W || y >= R.H) return false;
     uint32_t sample = R.spp_start + s_local, branch = 0u;
     if (R.subs) {  // branch schedule (C20): the pass's sample key and this item's branch
@@ -2020,7 +2026,7 @@ __device__ __forceinline__ bool item_path(const DevCamera &C, const DevRender &R
         sample = sb.x;
         branch = sb.y >> 16;
     }
-    new_path(C, R, y * R.W + x, sample, ps);
+    new_path(C, R, x, y, sample, ps);
     ps.branch = branch;
     begin_segment(ps);  // first segment: never capped
     return true;
@@ -2032,16 +2038,14 @@ __device__ __forceinline__ bool item_path(const DevCamera &C, const DevRender &R
 template <bool kSeed = false>
 __device__ inline bool seed_item(const DevCamera &C, const DevRender &R, const WaveBuffers &B, uint32_t slot,
                                  uint32_t item, PathState &ps, Counters &cnt) {
-    if (!item_path(C, R, item, ps)) {
+    uint32_t x, y;
+    if (!item_path(C, R, item, ps, x, y)) {
         B.color[item] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         return false;
     }
     cnt.paths++;
-    if (R.beam) {  // the camera ray's beam start (its tile's, beam_kernel)
-        uint32_t x, y;
-        item_pixel(R, item % R.total_items, x, y);
+    if (R.beam)  // the camera ray's beam start (its tile's, beam_kernel)
         ps.beam = R.beam[(y / kBeamTile) * R.beam_tx + x / kBeamTile];
-    }
     if (kSeed) {
         if (!B.lean) B.item0[slot] = item;  // lean: the chunk's first shade takes item = slot
     } else {
@@ -2371,7 +2375,8 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     if (first) {
         item = kLean ? slot : B.item0[slot];
         PathState s0;
-        item_path(C, R, item, s0);  // the seed only queued items inside the image
+        uint32_t x, y;
+        item_path<false>(C, R, item, s0, x, y);  // the seed only queued items inside the image
         float4 a, b;
         uint2 c;
         pack_path(s0, item, a, b, c);
@@ -2460,10 +2465,13 @@ constexpr uint32_t kShadeLdsBlocks = OCTPT_SHADE_LDS_BLOCKS;
 // every item); the instance without it is 19 VGPRs leaner (96 instead of 115, 5 waves/SIMD instead of 4).
 // kMode: 0 = the 40-B path state, no regeneration; 1 = with regeneration; 2 = the lean 24-B path state (no
 // regeneration, no sun sampling, kLean above)
-template <bool kNee, bool kLdsMats, int kMode>
+// kNoFirst (OCTPT_SHADE_FIRST_SPLIT): an instance for the chunk's later launches, compiled without the first
+// launch's path-state rebuild (first is 0)
+template <bool kNee, bool kLdsMats, int kMode, bool kNoFirst = false>
 __global__ __launch_bounds__(kBlock, kMode == 2 ? OCTPT_SHADE_LEAN_WAVES : OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
-                                                          uint32_t q, uint32_t chunk_items, uint32_t first,
+                                                          uint32_t q, uint32_t chunk_items, uint32_t first_arg,
                                                           unsigned long long *__restrict__ stats) {
+    const uint32_t first = kNoFirst ? 0u : first_arg;
     constexpr uint32_t kT = (kLdsMats && kShadeLdsMats) ? kShadeLdsMats : 1u;
     __shared__ DevMaterial smats[kT];
     __shared__ DevTexture stexs[kT];
@@ -2749,8 +2757,9 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
     const uint32_t i = blockIdx.x * (64u / kBeamLanes) + grp;
     if (i >= n_tiles) return;  // whole groups leave: the shuffles below stay inside a group
     const uint32_t rt = dealt_tile(R.tile_order, R.shard_index + (i / kBeamSub) * R.shard_count), sub = i % kBeamSub;
-    const uint32_t x0 = (rt % R.tiles_x) * kTile + (sub % (kTile / kBeamTile)) * kBeamTile,
-                   y0 = (rt / R.tiles_x) * kTile + (sub / (kTile / kBeamTile)) * kBeamTile;
+    const uint32_t rty = udiv_c(rt, R.div_tiles_x);
+    const uint32_t x0 = (rt - rty * R.tiles_x) * kTile + (sub % (kTile / kBeamTile)) * kBeamTile,
+                   y0 = rty * kTile + (sub / (kTile / kBeamTile)) * kBeamTile;
     if (x0 >= R.W || y0 >= R.H) return;  // no pixel of the image: never read
     const uint32_t tile = (y0 / kBeamTile) * R.beam_tx + x0 / kBeamTile;
     const uint32_t x1 = min(x0 + kBeamTile, R.W), y1 = min(y0 + kBeamTile, R.H);
@@ -2870,8 +2879,9 @@ __global__ __launch_bounds__(64) void beam_kernel(DevScene S, DevCamera C, DevRe
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i >= n_tiles) return;
     const uint32_t rt = dealt_tile(R.tile_order, R.shard_index + (i / kBeamSub) * R.shard_count), sub = i % kBeamSub;
-    const uint32_t x0 = (rt % R.tiles_x) * kTile + (sub % (kTile / kBeamTile)) * kBeamTile,
-                   y0 = (rt / R.tiles_x) * kTile + (sub / (kTile / kBeamTile)) * kBeamTile;
+    const uint32_t rty = udiv_c(rt, R.div_tiles_x);
+    const uint32_t x0 = (rt - rty * R.tiles_x) * kTile + (sub % (kTile / kBeamTile)) * kBeamTile,
+                   y0 = rty * kTile + (sub / (kTile / kBeamTile)) * kBeamTile;
     if (x0 >= R.W || y0 >= R.H) return;  // no pixel of the image: never read
     const uint32_t tile = (y0 / kBeamTile) * R.beam_tx + x0 / kBeamTile;
     const uint32_t x1 = min(x0 + kBeamTile, R.W), y1 = min(y0 + kBeamTile, R.H);
@@ -3089,18 +3099,24 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
     return hipGetLastError();
 }
 
-// the shade instance a scene and chunk launch (sun sampling, LDS material tables, regeneration, lean state)
+#ifndef OCTPT_SHADE_FIRST_SPLIT
+#define OCTPT_SHADE_FIRST_SPLIT 0
+#endif
+// the shade instance a scene and chunk launch (sun sampling, LDS material tables, regeneration, lean state; with
+// OCTPT_SHADE_FIRST_SPLIT the lean state's later launches, first == false, take the instance without the rebuild)
 template <bool kNee, bool kLds>
-static const void *shade_instance_of(int mode) {
-    if (!kNee && mode == 2) return reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2>);
+static const void *shade_instance_of(int mode, bool first) {
+    if (!kNee && mode == 2)
+        return (OCTPT_SHADE_FIRST_SPLIT && !first) ? reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2, true>)
+                                                    : reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2>);
     return mode == 1 ? reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, 1>)
                      : reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, 0>);
 }
 bool shade_lds_tables(const DevScene &S) { return S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats; }
-static const void *shade_instance(const DevScene &S, int mode) {
+static const void *shade_instance(const DevScene &S, int mode, bool first = false) {
     const bool lds = shade_lds_tables(S);
-    return S.sun.sun_sampling ? (lds ? shade_instance_of<true, true>(mode) : shade_instance_of<true, false>(mode))
-                              : (lds ? shade_instance_of<false, true>(mode) : shade_instance_of<false, false>(mode));
+    return S.sun.sun_sampling ? (lds ? shade_instance_of<true, true>(mode, first) : shade_instance_of<true, false>(mode, first))
+                              : (lds ? shade_instance_of<false, true>(mode, first) : shade_instance_of<false, false>(mode, first));
 }
 
 int shade_blocks_per_cu(const DevScene &S, int mode) {
@@ -3116,8 +3132,8 @@ hipError_t launch_wf_shade(const DevScene &S, const DevCamera &C, const DevRende
     uint32_t first_u = first;
     void *args[] = {const_cast<DevScene *>(&S), const_cast<DevCamera *>(&C), const_cast<DevRender *>(&R),
                     const_cast<WaveBuffers *>(&B), &q, &chunk_items, &first_u, &stats};
-    const hipError_t e = hipLaunchKernel(shade_instance(S, shade_mode(regen, B.lean != 0u)), dim3(grid), dim3(kBlock),
-                                         args, 0, stream);
+    const hipError_t e = hipLaunchKernel(shade_instance(S, shade_mode(regen, B.lean != 0u), first != 0u), dim3(grid),
+                                         dim3(kBlock), args, 0, stream);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }
