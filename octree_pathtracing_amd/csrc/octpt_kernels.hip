@@ -715,10 +715,11 @@ __device__ inline void commit_block_hit(const DevScene &S, PathState &r, uint32_
 }
 
 // Chunky-style commit [C1]: the ray origin moves to the hit point
-// kSphOnly: a sphere-only scene's shade instance (no box, block-model or block-value code compiled in)
-template <bool kSphOnly = false>
+// kSP: the primitive kinds of the scene a shade instance serves (kPrims*: spheres only; boxes without block models;
+// block values only; kPrimsModels = any scene), so that a scene's instance carries no other kind's code
+template <int kSP = kPrimsModels>
 __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim, const PrimHit &h, Counters &cnt) {
-    if (!kSphOnly && S.has_blocks) {
+    if (kSP == kPrimsBlocks || (kSP == kPrimsModels && S.has_blocks)) {
         commit_block_hit(S, r, prim, h.t, h.u, h.v, cnt);
         return;
     }
@@ -727,7 +728,7 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
     uint32_t mat;
     v3 n;
     bool uv_ready;
-    if (kSphOnly || !(prim & kPrimCuboidBit)) {
+    if (kSP == kPrimsSpheres || !(prim & kPrimCuboidBit)) {
         const float4 sp = S.spheres[prim];
         n = V((p.x - sp.x) / sp.w, (p.y - sp.y) / sp.w, (p.z - sp.z) / sp.w);
         mat = S.sphere_mat[prim];
@@ -740,7 +741,7 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
         const uint32_t axis = h.axis();
         const float nsgn = h.nsgn();
         mat = S.cub_mat[6u * ci + face_index(axis, nsgn)];
-        const uint32_t mdl = S.has_models ? S.cub_model[ci] : OCTPT_MODEL_NONE;
+        const uint32_t mdl = (kSP == kPrimsModels && S.has_models) ? S.cub_model[ci] : OCTPT_MODEL_NONE;
         if (mdl != OCTPT_MODEL_NONE) {
             // block-model hit [C19]: the hit record holds the instance and t; the quad is the one
             // model_test chose, found again by the same computation with t_next = t
@@ -2367,7 +2368,7 @@ __global__ __launch_bounds__(kBlock, OCTPT_EXTEND_WAVES_OF(kPrims)) void wf_exte
 // through the same pack / unpack as a stored path, instead of being read.
 // kLean with OCTPT_LEAN_POS: the state is read at (q, pos) and a continuing path's is not stored here: the caller
 // stores it at the position its next ray takes (store_lean_at).
-template <bool kNee, bool kLean = false, bool kSphOnly = false>
+template <bool kNee, bool kLean = false, int kSP = kPrimsModels>
 __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C, const DevRender &R,
                                            const WaveBuffers &B, bool first, float4 r0, float4 r1, const uint2 *hit_rec,
                                            const uint4 *hit4_rec, PathState &ps, uint32_t &slot, uint32_t &item,
@@ -2393,7 +2394,8 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     // the hit record: 8 B, or in block-value scenes (a uniform branch) 16 B with its (u, v) (C23)
     uint2 hr;
     float2 huv = make_float2(0.0f, 0.0f);
-    if (!kSphOnly && S.has_blocks) {
+    constexpr bool kMayBlocks = kSP == kPrimsBlocks || kSP == kPrimsModels;
+    if (kSP == kPrimsBlocks || (kMayBlocks && S.has_blocks)) {
         const uint4 r = *hit4_rec;
         hr = make_uint2(r.x, r.y);
         huv = make_float2(__uint_as_float(r.z), __uint_as_float(r.w));
@@ -2413,7 +2415,7 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     const bool was_shadow = kNee && ps.shadow;
     if (was_shadow) load_nee(B, slot, ps);
     const bool hit = hr.x != kPrimNone;
-    if (!kSphOnly && hit && S.has_blocks) {  // block-value leaf (C23): the record's (u, v) beside it
+    if (hit && (kSP == kPrimsBlocks || (kMayBlocks && S.has_blocks))) {  // block-value leaf (C23): (u, v) beside it
         ps.n = V(0.0f, 0.0f, 0.0f);
         commit_block_hit(S, ps, hr.x, __uint_as_float(hr.y), huv.x, huv.y, cnt);
     } else if (hit) {
@@ -2422,9 +2424,10 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
         h.t = __uint_as_float(hr.y);
         h.f = flags;
         // a sphere hit record carries its root, decided by extend's estimate: t exactly
-        if (kSphOnly || !(hr.x & kPrimCuboidBit)) h.t = sphere_root(S.spheres[hr.x & kPrimIndexMask], ps.o, ps.d, flags & 1u);
+        if (kSP == kPrimsSpheres || !(hr.x & kPrimCuboidBit))
+            h.t = sphere_root(S.spheres[hr.x & kPrimIndexMask], ps.o, ps.d, flags & 1u);
         ps.n = V(0.0f, 0.0f, 0.0f);
-        commit_hit<kSphOnly>(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
+        commit_hit<kSP>(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
     }
     bool cont = shade_segment<kNee>(S, R, ps, hit, cnt);
     if (cont) cont = begin_segment(ps);
@@ -2469,7 +2472,7 @@ constexpr uint32_t kShadeLdsBlocks = OCTPT_SHADE_LDS_BLOCKS;
 // regeneration, no sun sampling, kLean above)
 // kNoFirst (OCTPT_SHADE_FIRST_SPLIT): an instance for the chunk's later launches, compiled without the first
 // launch's path-state rebuild (first is 0)
-template <bool kNee, bool kLdsMats, int kMode, bool kNoFirst = false, bool kSphOnly = false>
+template <bool kNee, bool kLdsMats, int kMode, bool kNoFirst = false, int kSP = kPrimsModels>
 __global__ __launch_bounds__(kBlock, kMode == 2 ? OCTPT_SHADE_LEAN_WAVES : OCTPT_SHADE_WAVES) void wf_shade_kernel(DevScene Sg, DevCamera C, DevRender R, WaveBuffers B,
                                                           uint32_t q, uint32_t chunk_items, uint32_t first_arg,
                                                           unsigned long long *__restrict__ stats) {
@@ -2519,7 +2522,7 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? OCTPT_SHADE_LEAN_WAVES : OCTPT
                 cam_ray(B.eye, shard_lo(seg, chunk_items) + base + lane, r0c, r1);
             }
             const float4 r0 = first ? B.eye : B.ray0[q][i];  // (the chunk's first shade: the seed's camera rays)
-            append = shade_lane<kNee, kMode == 2, kSphOnly>(S, C, R, B, first != 0u, r0, r1, B.hit + i,
+            append = shade_lane<kNee, kMode == 2, kSP>(S, C, R, B, first != 0u, r0, r1, B.hit + i,
                                                   S.has_blocks ? B.hit4 + i : nullptr, ps, slot, item, cnt, q, i);
             finished = !append;
         }
@@ -3106,18 +3109,21 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
 #endif
 // the shade instance a scene and chunk launch (sun sampling, LDS material tables, regeneration, lean state; with
 // OCTPT_SHADE_FIRST_SPLIT the lean state's later launches, first == false, take the instance without the rebuild)
-#ifndef OCTPT_SHADE_SPH_ONLY
-#define OCTPT_SHADE_SPH_ONLY 0
+#ifndef OCTPT_SHADE_PRIMS
+#define OCTPT_SHADE_PRIMS 1  // round 6: the lean instance per primitive kind (C3 +0.15..0.35 %, profiles/r06/shade_prims_ab.txt)
 #endif
+template <bool kLds, int kSP>
+static const void *lean_shade_of(bool first) {
+    return (OCTPT_SHADE_FIRST_SPLIT && !first) ? reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2, true, kSP>)
+                                                : reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2, false, kSP>);
+}
 template <bool kNee, bool kLds>
-static const void *shade_instance_of(int mode, bool first, bool sph_only) {
-    if (!kNee && mode == 2) {
-        if (OCTPT_SHADE_SPH_ONLY && sph_only)  // sphere-only scenes (C2, C3): the lean instance without box / block code
-            return (OCTPT_SHADE_FIRST_SPLIT && !first)
-                       ? reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2, true, true>)
-                       : reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2, false, true>);
-        return (OCTPT_SHADE_FIRST_SPLIT && !first) ? reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2, true>)
-                                                    : reinterpret_cast<const void *>(wf_shade_kernel<false, kLds, 2>);
+static const void *shade_instance_of(int mode, bool first, int prims) {
+    if (!kNee && mode == 2) {  // the lean instances: per primitive kind (OCTPT_SHADE_PRIMS) and by launch (first)
+        if (OCTPT_SHADE_PRIMS && prims == kPrimsSpheres) return lean_shade_of<kLds, kPrimsSpheres>(first);
+        if (OCTPT_SHADE_PRIMS && prims == kPrimsBoxes) return lean_shade_of<kLds, kPrimsBoxes>(first);
+        if (OCTPT_SHADE_PRIMS && prims == kPrimsBlocks) return lean_shade_of<kLds, kPrimsBlocks>(first);
+        return lean_shade_of<kLds, kPrimsModels>(first);
     }
     return mode == 1 ? reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, 1>)
                      : reinterpret_cast<const void *>(wf_shade_kernel<kNee, kLds, 0>);
@@ -3125,10 +3131,10 @@ static const void *shade_instance_of(int mode, bool first, bool sph_only) {
 bool shade_lds_tables(const DevScene &S) { return S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats; }
 static const void *shade_instance(const DevScene &S, int mode, bool first = false) {
     const bool lds = shade_lds_tables(S);
-    const bool sph = !S.has_cuboids && !S.has_models && !S.has_blocks;
+    const int prims = S.has_blocks ? kPrimsBlocks : S.has_models ? kPrimsModels : S.has_cuboids ? kPrimsBoxes : kPrimsSpheres;
     return S.sun.sun_sampling
-               ? (lds ? shade_instance_of<true, true>(mode, first, sph) : shade_instance_of<true, false>(mode, first, sph))
-               : (lds ? shade_instance_of<false, true>(mode, first, sph) : shade_instance_of<false, false>(mode, first, sph));
+               ? (lds ? shade_instance_of<true, true>(mode, first, prims) : shade_instance_of<true, false>(mode, first, prims))
+               : (lds ? shade_instance_of<false, true>(mode, first, prims) : shade_instance_of<false, false>(mode, first, prims));
 }
 
 int shade_blocks_per_cu(const DevScene &S, int mode) {
