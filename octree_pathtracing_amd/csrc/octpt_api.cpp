@@ -596,6 +596,9 @@ octpt_status upload_tables(octpt_ctx *ctx, const octpt_scene_desc *d, bool host_
     S.n_mats = d->material_count;
     S.texs = d_texs;
     S.n_texs = d->texture_count;
+    S.has_images = 0u;
+    for (uint32_t t = 0; t < d->texture_count; ++t)
+        if (d->textures[t].kind == OCTPT_TEXTURE_IMAGE) S.has_images = 1u;
     S.texels = d_texels;
     S.lut_float = ctx->d_lut_float;
     make_sun(d->sun, lf, S.sun);
@@ -1042,7 +1045,8 @@ octpt_status enqueue_wavefront(octpt_ctx *ctx, const DevRender &R, float4 *d_acc
         const uint32_t n_seed = (uint32_t)std::min<uint64_t>(pool, chunk_items);
         const bool regen = n_seed < chunk_items;  // else the seed claimed every item of the chunk
         // the lean 24-B path state: L stays 0 until the path ends, item = slot
-        ctx->wb.lean = (!regen && ctx->lean_scene && !ctx->no_lean) ? 1u : 0u;
+        // (and, OCTPT_LEAN_STRICT, no branch schedule: the lean shade instances carry no first-reflection split)
+        ctx->wb.lean = (!regen && ctx->lean_scene && !ctx->no_lean && !(OCTPT_LEAN_STRICT && R.subs)) ? 1u : 0u;
         const int grid_shade = grid_shade_of(shade_mode(regen, ctx->wb.lean != 0u));
         // the seed writes its camera rays as 16-B records (store_cam_ray) when every item has its pixel: the first
         // extend (cam) and shade (first = 2) decode them

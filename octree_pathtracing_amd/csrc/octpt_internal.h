@@ -126,6 +126,7 @@ struct DevScene {
     const float *lut_float;         // LUT_TABLE_FLOAT (texture.rs:51-54)
     DevSun sun;
     int32_t emitters;
+    uint32_t has_images;  // some texture is an image (shade's colour-only instance when not)
 };
 
 struct DevCamera {
@@ -227,6 +228,10 @@ struct WaveBuffers {
     // pool holding the chunk (item = slot), set per chunk by the host
     uint32_t lean;
 };
+// the lean path state's chunks exclude branch schedules (C20) as well as emission and sun sampling (A/B knob)
+#ifndef OCTPT_LEAN_STRICT
+#define OCTPT_LEAN_STRICT 1
+#endif
 // shade instance: 0 = 40-B path state, 1 = with regeneration (pool smaller than the chunk), 2 = lean
 inline int shade_mode(bool regen, bool lean) { return regen ? 1 : (lean ? 2 : 0); }
 

@@ -716,7 +716,10 @@ __device__ inline void commit_block_hit(const DevScene &S, PathState &r, uint32_
 
 // Chunky-style commit [C1]: the ray origin moves to the hit point
 // kSP: the primitive kinds of the scene a shade instance serves (kPrims*: spheres only; boxes without block models;
-// block values only; kPrimsModels = any scene), so that a scene's instance carries no other kind's code
+// block values only; kPrimsModels = any scene; kShadeSphColour: spheres only and colour textures only), so that a
+// scene's instance carries no other kind's code
+constexpr int kShadeSphColour = 4;
+constexpr bool sph_kind(int k) { return k == kPrimsSpheres || k == kShadeSphColour; }
 template <int kSP = kPrimsModels>
 __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim, const PrimHit &h, Counters &cnt) {
     if (kSP == kPrimsBlocks || (kSP == kPrimsModels && S.has_blocks)) {
@@ -728,7 +731,7 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
     uint32_t mat;
     v3 n;
     bool uv_ready;
-    if (kSP == kPrimsSpheres || !(prim & kPrimCuboidBit)) {
+    if (sph_kind(kSP) || !(prim & kPrimCuboidBit)) {
         const float4 sp = S.spheres[prim];
         n = V((p.x - sp.x) / sp.w, (p.y - sp.y) / sp.w, (p.z - sp.z) / sp.w);
         mat = S.sphere_mat[prim];
@@ -790,7 +793,7 @@ __device__ inline void commit_hit(const DevScene &S, PathState &r, uint32_t prim
     } else {
         r.cur = mat;
         const DevMaterial &m = S.mats[mat];
-        if (m.texture_kind == 0u) {
+        if (kSP == kShadeSphColour || m.texture_kind == 0u) {  // (a colour-only scene's instance has no image path)
             r.col[0] = m.color[0];
             r.col[1] = m.color[1];
             r.col[2] = m.color[2];
@@ -1514,7 +1517,9 @@ __device__ inline void shadow_segment_done(const DevScene &S, PathState &ray, bo
 // path_tracer.rs:15-135 in forward-throughput form, from a finished segment to either the
 // next segment's ray (returns true) or the end of the path (returns false).  kNee: the scene may
 // sample the sun; shadow segments run between a diffuse hit and its bounce.
-template <bool kNee>
+// kLean: the lean path state's chunks (no emitting material, no branch schedule: enqueue_wavefront's lean rule), whose
+// instances carry neither the emission term nor the first reflection's split
+template <bool kNee, bool kLean = false>
 __device__ inline bool shade_segment(const DevScene &S, const DevRender &R, PathState &ray, bool hit,
                                      Counters &cnt) {
     if (kNee && ray.shadow) {
@@ -1537,7 +1542,7 @@ __device__ inline bool shade_segment(const DevScene &S, const DevRender &R, Path
     }
     if (ray.depth + 1u >= R.max_depth) return false;
     ray.depth += 1u;
-    if (ray.depth == 1u && ray.branch != 0u) {  // the first reflection splits (path_tracer.rs:66) [C20]
+    if (!(OCTPT_LEAN_STRICT && kLean) && ray.depth == 1u && ray.branch != 0u) {  // the first reflection splits [C20]
         ray.rng = branch_state(ray.rng, ray.branch);
         ray.seg_base = ray.path_segs;
     }
@@ -1549,7 +1554,7 @@ __device__ inline bool shade_segment(const DevScene &S, const DevRender &R, Path
         if (do_metal) T = V(T.x * ray.col[0], T.y * ray.col[1], T.z * ray.col[2]);
         specular_reflection(ray, m.roughness);
     } else if (rng_next(ray.rng) < diffuse) {
-        if (S.emitters && m.emittance > RAY_EPSILON) {
+        if (!(OCTPT_LEAN_STRICT && kLean) && S.emitters && m.emittance > RAY_EPSILON) {
             const v3 e = V(ray.col[0] * ray.col[0] * m.emittance, ray.col[1] * ray.col[1] * m.emittance,
                            ray.col[2] * ray.col[2] * m.emittance);
             ray.L = V(ray.L.x + T.x * e.x, ray.L.y + T.y * e.y, ray.L.z + T.z * e.z);
@@ -2424,12 +2429,12 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
         h.t = __uint_as_float(hr.y);
         h.f = flags;
         // a sphere hit record carries its root, decided by extend's estimate: t exactly
-        if (kSP == kPrimsSpheres || !(hr.x & kPrimCuboidBit))
+        if (sph_kind(kSP) || !(hr.x & kPrimCuboidBit))
             h.t = sphere_root(S.spheres[hr.x & kPrimIndexMask], ps.o, ps.d, flags & 1u);
         ps.n = V(0.0f, 0.0f, 0.0f);
         commit_hit<kSP>(S, ps, (hr.x & kPrimCuboidBit) | (hr.x & kPrimIndexMask), h, cnt);
     }
-    bool cont = shade_segment<kNee>(S, R, ps, hit, cnt);
+    bool cont = shade_segment<kNee, kLean>(S, R, ps, hit, cnt);
     if (cont) cont = begin_segment(ps);
     if (cont) {
         if (!kPos) store_path<kLean>(B, slot, ps, item);
@@ -2441,7 +2446,8 @@ __device__ __forceinline__ bool shade_lane(const DevScene &S, const DevCamera &C
     }
     // segments this item reports (a branch > 0 reports none of the replayed prefix) and whether the
     // first reflection split (C20)
-    const uint32_t segs = ps.branch == 0u ? ps.path_segs : (ps.depth ? ps.path_segs - ps.seg_base : 0u);
+    const uint32_t segs = ((OCTPT_LEAN_STRICT && kLean) || ps.branch == 0u) ? ps.path_segs
+                                                                             : (ps.depth ? ps.path_segs - ps.seg_base : 0u);
     B.color[item] = make_float4(ps.L.x, ps.L.y, ps.L.z, __uint_as_float(segs | (ps.depth ? 0x80000000u : 0u)));
     return false;
 }
@@ -3109,6 +3115,9 @@ hipError_t launch_wf_extend(const DevScene &S, const WaveBuffers &B, uint32_t q,
 #endif
 // the shade instance a scene and chunk launch (sun sampling, LDS material tables, regeneration, lean state; with
 // OCTPT_SHADE_FIRST_SPLIT the lean state's later launches, first == false, take the instance without the rebuild)
+#ifndef OCTPT_SHADE_COLOUR
+#define OCTPT_SHADE_COLOUR 1  // sphere scenes with colour textures only get an instance without the image path (A/B knob)
+#endif
 #ifndef OCTPT_SHADE_PRIMS
 #define OCTPT_SHADE_PRIMS 1  // round 6: the lean instance per primitive kind (C3 +0.15..0.35 %, profiles/r06/shade_prims_ab.txt)
 #endif
@@ -3120,6 +3129,7 @@ static const void *lean_shade_of(bool first) {
 template <bool kNee, bool kLds>
 static const void *shade_instance_of(int mode, bool first, int prims) {
     if (!kNee && mode == 2) {  // the lean instances: per primitive kind (OCTPT_SHADE_PRIMS) and by launch (first)
+        if (OCTPT_SHADE_PRIMS && prims == kShadeSphColour) return lean_shade_of<kLds, kShadeSphColour>(first);
         if (OCTPT_SHADE_PRIMS && prims == kPrimsSpheres) return lean_shade_of<kLds, kPrimsSpheres>(first);
         if (OCTPT_SHADE_PRIMS && prims == kPrimsBoxes) return lean_shade_of<kLds, kPrimsBoxes>(first);
         if (OCTPT_SHADE_PRIMS && prims == kPrimsBlocks) return lean_shade_of<kLds, kPrimsBlocks>(first);
@@ -3131,7 +3141,11 @@ static const void *shade_instance_of(int mode, bool first, int prims) {
 bool shade_lds_tables(const DevScene &S) { return S.n_mats <= kShadeLdsMats && S.n_texs <= kShadeLdsMats; }
 static const void *shade_instance(const DevScene &S, int mode, bool first = false) {
     const bool lds = shade_lds_tables(S);
-    const int prims = S.has_blocks ? kPrimsBlocks : S.has_models ? kPrimsModels : S.has_cuboids ? kPrimsBoxes : kPrimsSpheres;
+    const int prims = S.has_blocks    ? kPrimsBlocks
+                      : S.has_models  ? kPrimsModels
+                      : S.has_cuboids ? kPrimsBoxes
+                      : S.has_images  ? kPrimsSpheres
+                                      : (OCTPT_SHADE_COLOUR ? kShadeSphColour : kPrimsSpheres);
     return S.sun.sun_sampling
                ? (lds ? shade_instance_of<true, true>(mode, first, prims) : shade_instance_of<true, false>(mode, first, prims))
                : (lds ? shade_instance_of<false, true>(mode, first, prims) : shade_instance_of<false, false>(mode, first, prims));
