@@ -1090,6 +1090,14 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
                                 uint32_t &prim, PrimHit &h) {
     // :128-130: max_dst = 1024 * 2^-depth > 0, so the reference's `max_dst >= 0` guard always holds
     const float max_dst = MAX_DST_WORLD * S.octree_scale;  // :75, wave-uniform
+#ifndef OCTPT_SETPRIO
+#define OCTPT_SETPRIO 1  // round 6: C3 +0.4..0.6 %, C4 +1.0..1.2 %; the block instances mixed (profiles/r06/setprio_ab.txt)
+#endif
+    // Wave priority around the node-slot load: a wave at the top of its step (about to issue the load its next
+    // iteration waits for) issues ahead of the waves in the rest of their step's arithmetic, so the SIMD's loads
+    // go out sooner (the sphere and box instances; the block instances measured mixed)
+    constexpr int kPrio = (kPrims == kPrimsSpheres || kPrims == kPrimsBoxes) ? OCTPT_SETPRIO : 0;
+    if constexpr (kPrio > 0) __builtin_amdgcn_s_setprio(kPrio);
     const bool stopped = esvo_capped(E.iter) | (E.t_min > max_dst);
     E.iter += stopped ? 0u : 1u;
     const v3 t_corner = vsub(vmul(E.pos, E.t_coef), E.t_bias);
@@ -1122,6 +1130,7 @@ __device__ inline int esvo_step(const DevScene &S, const TraceRay &ray, Esvo &E,
         lsph = S.leaf_sph[sidx];
         ISSUED(cnt, 16);
     }
+    if constexpr (kPrio > 0) __builtin_amdgcn_s_setprio(0);
 #ifdef OCTPT_PROFILE_LANES
     prof_wave(cnt.p_leaf_it, cnt.p_leaf_ln, take_leaf);
     prof_wave(cnt.p_push_it, cnt.p_desc_ln, descend);
